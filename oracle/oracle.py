@@ -1,0 +1,200 @@
+"""ctypes wrapper of the CPU oracle (liboracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this,
+and only as the checker / the timed CPU baseline.  The product path (libhbam.so)
+never loads it.  Parity status is documented in hbam_oracle.h and DESIGN.md §3.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+OR_OK, OR_EIO, OR_ETRUNC, OR_EFORMAT, OR_ERUNTIMEIO, OR_EEOF, OR_EREFID, OR_EDATA, OR_ENOMEM = (
+    0, -1, -2, -3, -4, -5, -6, -7, -8)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        u8p = C.POINTER(C.c_uint8)
+        L.or_murmurhash3.restype = C.c_int64
+        L.or_murmurhash3.argtypes = [u8p, C.c_int32, C.c_int32]
+        L.or_get_key.restype = C.c_int64
+        L.or_get_key.argtypes = [C.c_int32, C.c_int32, C.c_uint16, u8p, C.c_int32]
+        L.or_scan_blocks.restype = C.c_int64
+        L.or_scan_blocks.argtypes = [u8p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.or_inflate_block.restype = C.c_int
+        L.or_inflate_block.argtypes = [u8p, C.c_uint32, C.c_void_p, C.c_uint32,
+                                       C.POINTER(C.c_uint32), C.c_int]
+        L.or_read_header.restype = C.c_int
+        L.or_read_header.argtypes = [u8p, C.c_uint64, C.POINTER(OrHeader)]
+        L.or_guess_bam_record_start.restype = C.c_int64
+        L.or_guess_bam_record_start.argtypes = [u8p, C.c_uint64, C.c_int64, C.c_int64, C.c_int32,
+                                                C.POINTER(C.c_int)]
+        L.or_guess_bgzf_block_start.restype = C.c_int64
+        L.or_guess_bgzf_block_start.argtypes = [u8p, C.c_uint64, C.c_int64, C.c_int64,
+                                                C.POINTER(C.c_int)]
+        L.or_file_splits.restype = C.c_int64
+        L.or_file_splits.argtypes = [C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.or_probabilistic_splits.restype = C.c_int64
+        L.or_probabilistic_splits.argtypes = [u8p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
+                                              C.c_void_p, C.c_void_p]
+        L.or_splitting_index.restype = C.c_int64
+        L.or_splitting_index.argtypes = [u8p, C.c_uint64, C.c_int32, C.c_void_p, C.c_uint64]
+        L.or_read_split_cols.restype = C.c_int
+        L.or_read_split_cols.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_int,
+                                         C.POINTER(OrCols)]
+        L.or_cols_free.restype = None
+        L.or_cols_free.argtypes = [C.POINTER(OrCols)]
+        _LIB = L
+    return _LIB
+
+
+class OrHeader(C.Structure):
+    _fields_ = [("l_text", C.c_int32), ("n_ref", C.c_int32), ("header_ulen", C.c_uint64),
+                ("first_voffset", C.c_uint64)]
+
+
+class OrCols(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("status", C.c_int32), ("err_record", C.c_uint64),
+                ("voffset", C.POINTER(C.c_uint64)), ("key", C.POINTER(C.c_int64)),
+                ("block_size", C.POINTER(C.c_int32)), ("ref_id", C.POINTER(C.c_int32)),
+                ("pos", C.POINTER(C.c_int32)), ("l_read_name", C.POINTER(C.c_uint8)),
+                ("mapq", C.POINTER(C.c_uint8)), ("bin", C.POINTER(C.c_uint16)),
+                ("n_cigar", C.POINTER(C.c_uint16)), ("flag", C.POINTER(C.c_uint16)),
+                ("l_seq", C.POINTER(C.c_int32)), ("next_ref_id", C.POINTER(C.c_int32)),
+                ("next_pos", C.POINTER(C.c_int32)), ("tlen", C.POINTER(C.c_int32)),
+                ("var_off", C.POINTER(C.c_uint64)), ("var", C.POINTER(C.c_uint8)),
+                ("cap", C.c_uint64), ("var_cap", C.c_uint64)]
+
+
+FIXED_FIELDS = [("voffset", np.uint64), ("key", np.int64), ("block_size", np.int32),
+                ("ref_id", np.int32), ("pos", np.int32), ("l_read_name", np.uint8),
+                ("mapq", np.uint8), ("bin", np.uint16), ("n_cigar", np.uint16),
+                ("flag", np.uint16), ("l_seq", np.int32), ("next_ref_id", np.int32),
+                ("next_pos", np.int32), ("tlen", np.int32)]
+
+
+def _buf(data):
+    """uint8 pointer to a bytes-like / numpy buffer (kept alive by the caller)."""
+    a = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    return a, a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def murmurhash3(b, seed=0):
+    a, p = _buf(bytes(b) if len(b) else b"\0")
+    return lib().or_murmurhash3(p, len(b), seed)
+
+
+def get_key(ref_id, pos0, flag, var):
+    a, p = _buf(bytes(var) if len(var) else b"\0")
+    return lib().or_get_key(ref_id, pos0, flag, p, len(var))
+
+
+def scan_blocks(data):
+    a, p = _buf(data)
+    cap = len(a) // 26 + 2
+    coff = np.zeros(cap, np.uint64)
+    clen = np.zeros(cap, np.uint32)
+    isz = np.zeros(cap, np.uint32)
+    crc = np.zeros(cap, np.uint32)
+    bad = C.c_uint64(0)
+    n = lib().or_scan_blocks(p, len(a), coff.ctypes.data, clen.ctypes.data, isz.ctypes.data,
+                             crc.ctypes.data, cap, C.byref(bad))
+    if n < 0:
+        return n, int(bad.value)
+    return dict(coff=coff[:n], clen=clen[:n], isize=isz[:n], crc=crc[:n])
+
+
+def inflate_block(blk, check_crc=True):
+    a, p = _buf(blk)
+    out = np.zeros(1 << 16, np.uint8)
+    ol = C.c_uint32(0)
+    rc = lib().or_inflate_block(p, len(a), out.ctypes.data, len(out), C.byref(ol), int(check_crc))
+    return rc, bytes(out[:ol.value]) if rc == 0 else b""
+
+
+def read_header(data):
+    a, p = _buf(data)
+    h = OrHeader()
+    rc = lib().or_read_header(p, len(a), C.byref(h))
+    if rc:
+        return rc
+    return dict(l_text=h.l_text, n_ref=h.n_ref, header_ulen=h.header_ulen,
+                first_voffset=h.first_voffset)
+
+
+def read_split(data, v_start, v_end, check_crc=False, keep_var=True):
+    """BAMRecordReader over one FileVirtualSplit -> dict of numpy columns."""
+    a, p = _buf(data)
+    c = OrCols()
+    lib().or_read_split_cols(p, len(a), v_start, v_end, int(check_crc), int(keep_var), C.byref(c))
+    n = int(c.n)
+    out = dict(n=n, status=int(c.status), err_record=int(c.err_record))
+    for name, dt in FIXED_FIELDS:
+        ptr = getattr(c, name)
+        out[name] = (np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt).copy() if n
+                     else np.zeros(0, dt))
+    out["var_off"] = np.ctypeslib.as_array(c.var_off, shape=(n + 1,)).copy()
+    vl = int(out["var_off"][-1])
+    out["var"] = np.ctypeslib.as_array(c.var, shape=(vl,)).copy() if vl else np.zeros(0, np.uint8)
+    lib().or_cols_free(C.byref(c))
+    return out
+
+
+def guess_bam_record_start(data, beg, end, n_ref):
+    a, p = _buf(data)
+    err = C.c_int(0)
+    r = lib().or_guess_bam_record_start(p, len(a), beg, end, n_ref, C.byref(err))
+    return r, err.value
+
+
+def guess_bgzf_block_start(data, beg, end):
+    a, p = _buf(data)
+    err = C.c_int(0)
+    r = lib().or_guess_bgzf_block_start(p, len(a), beg, end, C.byref(err))
+    return r, err.value
+
+
+def file_splits(file_len, split_size):
+    cap = file_len // max(split_size, 1) + 4
+    b = np.zeros(cap, np.uint64)
+    e = np.zeros(cap, np.uint64)
+    n = lib().or_file_splits(file_len, split_size, b.ctypes.data, e.ctypes.data, cap)
+    return b[:n], e[:n]
+
+
+def probabilistic_splits(data, beg, end):
+    a, p = _buf(data)
+    beg = np.ascontiguousarray(beg, np.uint64)
+    end = np.ascontiguousarray(end, np.uint64)
+    vs = np.zeros(len(beg), np.uint64)
+    ve = np.zeros(len(beg), np.uint64)
+    n = lib().or_probabilistic_splits(p, len(a), beg.ctypes.data, end.ctypes.data, len(beg),
+                                      vs.ctypes.data, ve.ctypes.data)
+    if n < 0:
+        return n
+    return vs[:n], ve[:n]
+
+
+def splitting_index(data, granularity=4096):
+    a, p = _buf(data)
+    cap = 1 << 20
+    out = np.zeros(cap, np.uint64)
+    n = lib().or_splitting_index(p, len(a), granularity, out.ctypes.data, cap)
+    if n < 0:
+        return n
+    return out[:n]
