@@ -1,0 +1,1185 @@
+// hbam_capi.hip — host runtime + C ABI (include/hbam.h) of the MI355X BAM read path.
+//
+// One context = one device + one HIP stream + grow-only device work buffers.  The
+// per-split pipeline (hbam_decode_split) is:
+//   K1 scan chunks -> gather -> verify chain      (BGZF block table, device)
+//   K2 inflate (+ K2b CRC)                        (lane per block, device)
+//   K5 entry/walk/stitch/fix/emit                 (record starts + voffsets, device)
+//   K6/K7/K8 decode fixed fields, status, keys    (device)
+//   pools (names/CIGAR/SEQ/QUAL/AUX)              (device)
+// The host only decides control flow from a few downloaded scalars (chain end,
+// first bad block, first stop record) — the reference's exception semantics.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "hbam_internal.h"
+#include "hbam_kernels.hip"
+#include "hbam_guess.hip"
+
+using namespace hbam;
+
+namespace {
+
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+enum BufId {
+  B_COMP,
+  B_CHUNK_CNT,
+  B_CHUNK_BASE,
+  B_CHUNK_POS,
+  B_CAND,
+  B_BLK,
+  B_UOFF,
+  B_ISZ32,
+  B_UBUF,
+  B_LENS,
+  B_INFST,
+  B_CRC,
+  B_ENTRY,
+  B_EXIT,
+  B_REL,
+  B_COUNT,
+  B_RECBASE,
+  B_RECOFF,
+  B_VOFF,
+  B_SMALL,
+  B_PARTIAL,
+  B_EVENTS,
+  B_BADLIST,
+  // columns
+  B_C_STATUS,
+  B_C_BS,
+  B_C_REF,
+  B_C_POS,
+  B_C_LRN,
+  B_C_MAPQ,
+  B_C_BIN,
+  B_C_NCIG,
+  B_C_FLAG,
+  B_C_LSEQ,
+  B_C_NREF,
+  B_C_NPOS,
+  B_C_TLEN,
+  B_C_KEY,
+  B_C_LAYOUT,
+  B_C_NAMELEN,
+  B_C_CIGN,
+  B_C_SEQLEN,
+  B_C_AUXLEN,
+  B_C_NAMEOFF,
+  B_C_CIGOFF,
+  B_C_SEQOFF,
+  B_C_AUXOFF,
+  B_C_NAMES,
+  B_C_CIGARS,
+  B_C_SEQ,
+  B_C_QUAL,
+  B_C_AUX,
+  B_COUNT_ALL
+};
+
+}  // namespace
+
+struct hbam_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hbam_opts opts{};
+  std::string err;
+  Buf bufs[B_COUNT_ALL];
+  hipEvent_t ev[16];
+  hbam_timing timing{};
+  uint64_t* pinned_small = nullptr;  // host pinned scalars
+};
+
+namespace {
+
+int set_err(hbam_ctx* c, int code, const char* fmt, ...) {
+  char b[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(b, sizeof b, fmt, ap);
+  va_end(ap);
+  if (c) c->err = b;
+  return code;
+}
+
+#define HIPCHK(ctx, x)                                                                      \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess)                                                                   \
+      return set_err((ctx), HBAM_EDEVICE, "%s:%d %s: %s", __FILE__, __LINE__, #x,           \
+                     hipGetErrorString(e_));                                                \
+  } while (0)
+
+template <typename T>
+int ensure(hbam_ctx* c, BufId id, size_t count, T** out) {
+  size_t bytes = count * sizeof(T) + 64;
+  Buf& b = c->bufs[id];
+  if (b.cap < bytes) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = std::max(bytes, b.cap + b.cap / 2);
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      e = hipMalloc(&b.p, bytes);
+      want = bytes;
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        b.p = nullptr;
+        return set_err(c, HBAM_ENOMEM, "hipMalloc(%zu) failed for buffer %d", bytes, (int)id);
+      }
+    }
+    b.cap = want;
+  }
+  *out = (T*)b.p;
+  return HBAM_OK;
+}
+
+inline uint32_t grid_for(uint64_t n, uint32_t wg) { return (uint32_t)((n + wg - 1) / wg); }
+
+// stream-ordered synchronous copy (the context stream is non-blocking: a plain hipMemcpy
+// on the null stream would not wait for its kernels)
+hipError_t copy_sync(hbam_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind k) {
+  if (!bytes) return hipSuccess;
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, k, c->stream);
+  if (e != hipSuccess) return e;
+  return hipStreamSynchronize(c->stream);
+}
+
+// exclusive scan of n u32 values -> out[0..n] (out[n] = total); returns total via host
+template <typename T>
+int scan_exclusive(hbam_ctx* c, const T* in, uint64_t n, uint64_t* out, uint64_t* total_host) {
+  const uint64_t tiles = std::max<uint64_t>(1, (n + SCAN_TILE - 1) / SCAN_TILE);
+  uint64_t* partial;
+  int rc = ensure(c, B_PARTIAL, tiles + 1, &partial);
+  if (rc) return rc;
+  k_scan_reduce<T><<<(uint32_t)tiles, SCAN_WG, 0, c->stream>>>(in, n, partial);
+  k_scan_partials<<<1, SCAN_WG, 0, c->stream>>>(partial, tiles, partial + tiles);
+  k_scan_apply<T><<<(uint32_t)tiles, SCAN_WG, 0, c->stream>>>(in, n, partial, out);
+  HIPCHK(c, hipGetLastError());
+  if (total_host) {
+    HIPCHK(c, hipMemcpyAsync(c->pinned_small, out + n, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *total_host = c->pinned_small[0];
+  }
+  return HBAM_OK;
+}
+
+inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | p[1] << 8); }
+inline int32_t rd32(const uint8_t* p) {
+  return (int32_t)((uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 |
+                   (uint32_t)p[3] << 24);
+}
+
+// [htsjdk] BCIS.readBlock + BlockGunzipper header checks for a block that the device
+// chain does not accept, from up to 26 bytes at its position (`avail` bytes exist).
+int readblock_error(const uint8_t* h, uint64_t avail) {
+  if (avail == 0) return HBAM_EEOF;      // clean end of data
+  if (avail < 18) return HBAM_ERUNTIMEIO; // IOException "Premature end of file" (wrapped)
+  const uint32_t blen = (uint32_t)rd16(h + 16) + 1u;
+  if (blen < 18) return HBAM_ERUNTIMEIO;  // IOException "Unexpected compressed block length"
+  if (blen > avail) return HBAM_ETRUNC;   // FileTruncatedException
+  // inflateBlock: ISIZE < 0 -> RuntimeIOException; unzipBlock header checks
+  const int32_t isize = rd32(h + blen - 4);
+  if (isize < 0) return HBAM_ERUNTIMEIO;
+  if (!(h[0] == 0x1f && h[1] == 0x8b && h[2] == 8 && h[3] == 4)) return HBAM_EFORMAT;
+  if (rd16(h + 10) != 6) return HBAM_EFORMAT;
+  return HBAM_EFORMAT;
+}
+
+struct Chain {
+  std::vector<BlockRec> blocks;  // host copy only when the fast path fails
+  uint64_t nb = 0;
+  int32_t end_code = HBAM_EEOF;  // what reading past the last block raises
+  uint64_t end_pos = 0;          // comp offset where the chain ends
+};
+
+// K1: block table of the chain starting at comp offset `start` (must be a block start).
+// Device-resident result in B_BLK (nb entries).  end_code: HBAM_EEOF for a clean end of
+// file, a readBlock error code, or HBAM_EMORE when the window ends mid-chain.
+int build_chain(hbam_ctx* c, const uint8_t* dcomp, uint64_t comp_len, uint64_t start,
+                bool window_is_file_end, Chain* ch) {
+  ch->nb = 0;
+  if (start >= comp_len) {
+    ch->end_code = window_is_file_end ? HBAM_EEOF : HBAM_EMORE;
+    ch->end_pos = start;
+    return HBAM_OK;
+  }
+  const uint64_t span = comp_len - start;
+  const uint64_t nchunks = (span + SCAN_CHUNK - 1) / SCAN_CHUNK;
+  uint32_t* chunk_cnt;
+  uint64_t *chunk_base, *chunk_pos, *cand, *small;
+  BlockRec* blk;
+  int rc;
+  if ((rc = ensure(c, B_CHUNK_CNT, nchunks, &chunk_cnt))) return rc;
+  if ((rc = ensure(c, B_CHUNK_BASE, nchunks + 1, &chunk_base))) return rc;
+  if ((rc = ensure(c, B_CHUNK_POS, nchunks * SCAN_CAP, &chunk_pos))) return rc;
+  if ((rc = ensure(c, B_SMALL, 16, &small))) return rc;
+  HIPCHK(c, hipMemsetAsync(small, 0, 16 * 8, c->stream));
+  uint32_t* overflow = (uint32_t*)small;
+  uint32_t* nbad = (uint32_t*)small + 1;
+  k_scan_chunks<<<(uint32_t)nchunks, 256, 0, c->stream>>>(dcomp, start, comp_len, chunk_cnt,
+                                                          chunk_pos, overflow);
+  HIPCHK(c, hipGetLastError());
+  uint64_t ncand = 0;
+  if ((rc = scan_exclusive<uint32_t>(c, chunk_cnt, nchunks, chunk_base, &ncand))) return rc;
+  if ((rc = ensure(c, B_CAND, ncand + 1, &cand))) return rc;
+  if ((rc = ensure(c, B_BLK, ncand + 1, &blk))) return rc;
+  k_gather_cands<<<grid_for(nchunks, 256), 256, 0, c->stream>>>(chunk_cnt, chunk_base, chunk_pos,
+                                                                nchunks, cand);
+  if (ncand)
+    k_verify_chain<<<grid_for(ncand, 256), 256, 0, c->stream>>>(dcomp, cand, ncand, comp_len,
+                                                                 blk, nbad);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small, small, 16, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint32_t ovf = ((uint32_t*)c->pinned_small)[0];
+  const uint32_t bad = ((uint32_t*)c->pinned_small)[1];
+  if (ovf) return set_err(c, HBAM_EUNSUPPORTED, "too many BGZF magic candidates per chunk");
+  // download candidate list only if the fast path failed or to check the ends
+  uint64_t first = ~0ULL;
+  BlockRec last{};
+  if (ncand) {
+    HIPCHK(c, hipMemcpyAsync(c->pinned_small, cand, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->pinned_small + 2, blk + (ncand - 1), sizeof(BlockRec),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    first = c->pinned_small[0];
+    memcpy(&last, c->pinned_small + 2, sizeof last);
+  }
+  uint8_t hdr[32];
+  auto classify_end = [&](uint64_t pos) -> int32_t {
+    const uint64_t avail = comp_len - pos;
+    memset(hdr, 0, sizeof hdr);
+    const uint64_t nget = std::min<uint64_t>(avail, 32);
+    if (nget) {
+      if (copy_sync(c, hdr, dcomp + pos, nget, hipMemcpyDeviceToHost) != hipSuccess) return HBAM_EDEVICE;
+    }
+    if (avail == 0) return window_is_file_end ? HBAM_EEOF : HBAM_EMORE;
+    const uint32_t blen = nget >= 18 ? (uint32_t)rd16(hdr + 16) + 1u : 0u;
+    if (!window_is_file_end && (avail < 18 || blen > avail)) return HBAM_EMORE;
+    if (avail >= 18 && blen >= 18 && blen <= avail && blen > 32) {
+      // block header looks readable but was not accepted: classify with its footer
+      std::vector<uint8_t> full(blen + 8);
+      if (copy_sync(c, full.data(), dcomp + pos, blen, hipMemcpyDeviceToHost) != hipSuccess)
+        return HBAM_EDEVICE;
+      return readblock_error(full.data(), avail);
+    }
+    return readblock_error(hdr, avail);
+  };
+  if (first != start) {
+    // the split's first block is not a BGZF block htsjdk accepts
+    ch->nb = 0;
+    ch->end_pos = start;
+    ch->end_code = classify_end(start);
+    return HBAM_OK;
+  }
+  if (bad == 0 || (bad == 1 && last.coff + last.clen > comp_len)) {
+    // every link consistent (the last block may run past the window)
+    uint64_t nb = ncand;
+    if (last.coff + last.clen > comp_len) nb = ncand - 1;
+    ch->nb = nb;
+    ch->end_pos = (nb == ncand) ? last.coff + last.clen : last.coff;
+    ch->end_code = classify_end(ch->end_pos);
+    return HBAM_OK;
+  }
+  // slow path: walk the chain on the host over the candidate list
+  std::vector<uint64_t> hc(ncand);
+  std::vector<BlockRec> hb(ncand);
+  HIPCHK(c, hipMemcpyAsync(hc.data(), cand, ncand * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(hb.data(), blk, ncand * sizeof(BlockRec), hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<BlockRec> chain;
+  uint64_t p = start;
+  size_t idx = 0;
+  for (;;) {
+    auto it = std::lower_bound(hc.begin() + (long)idx, hc.end(), p);
+    if (it == hc.end() || *it != p) break;
+    idx = (size_t)(it - hc.begin());
+    const BlockRec& r = hb[idx];
+    if (r.coff + r.clen > comp_len || r.clen < 18) break;
+    chain.push_back(r);
+    p = r.coff + r.clen;
+  }
+  ch->nb = chain.size();
+  ch->end_pos = p;
+  ch->end_code = classify_end(p);
+  HIPCHK(c, hipMemcpyAsync(blk, chain.data(), chain.size() * sizeof(BlockRec),
+                           hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBAM_OK;
+}
+
+__global__ void k_isize32(const BlockRec* __restrict__ blk, uint64_t n, uint32_t* __restrict__ out,
+                          uint32_t* __restrict__ big) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = blk[i].isize;
+  out[i] = s <= 65536u ? s : 0u;
+  if (s > 65536u) atomicMin(big, (uint32_t)i);
+}
+
+__global__ void k_first_bad_block(const int32_t* __restrict__ st, const uint32_t* __restrict__ crc,
+                                  const BlockRec* __restrict__ blk, uint64_t n, int check_crc,
+                                  unsigned long long* __restrict__ first) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool bad = st[i] != INF_OK;
+  if (!bad && check_crc) bad = crc[i] != blk[i].crc;
+  if (bad) atomicMin(first, (unsigned long long)i);
+}
+
+__global__ void k_collect_empty(const BlockRec* __restrict__ blk, const uint64_t* __restrict__ uoff,
+                                uint64_t n, uint64_t* __restrict__ ev, uint32_t* __restrict__ nev,
+                                uint32_t cap) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (i >= n) return;
+  if (blk[i].isize == 0) {
+    const uint32_t k = atomicAdd(nev, 1u);
+    if (k < cap) ev[k] = uoff[i];
+  }
+}
+
+int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint64_t nb,
+                   const uint64_t* uoff, uint8_t* ubuf, int32_t* st, bool want_crc, uint32_t* crc) {
+  uint8_t* lens;
+  int rc;
+  if ((rc = ensure(c, B_LENS, nb * LENS_SLOT, &lens))) return rc;
+  if (nb)
+    k_inflate<<<grid_for(nb, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(dcomp, blk, uoff, (uint32_t)nb,
+                                                                     ubuf, lens, st);
+  HIPCHK(c, hipGetLastError());
+  if (want_crc && nb) {
+    k_crc32<<<grid_for(nb, 256), 256, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, crc);
+    HIPCHK(c, hipGetLastError());
+  }
+  return HBAM_OK;
+}
+
+}  // namespace
+
+// =====================================================================================
+extern "C" {
+
+hbam_ctx* hbam_create(int device_ordinal, const hbam_opts* opts) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return nullptr;
+  if (device_ordinal < 0 || device_ordinal >= ndev) return nullptr;
+  if (hipSetDevice(device_ordinal) != hipSuccess) return nullptr;
+  hbam_ctx* c = new hbam_ctx();
+  c->device = device_ordinal;
+  if (opts) c->opts = *opts;
+  else c->opts.validate_refs = 1;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  for (auto& e : c->ev) (void)hipEventCreate(&e);
+  if (hipHostMalloc((void**)&c->pinned_small, 4096, hipHostMallocDefault) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+void hbam_destroy(hbam_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& b : c->bufs)
+    if (b.p) (void)hipFree(b.p);
+  for (auto& e : c->ev) (void)hipEventDestroy(e);
+  if (c->pinned_small) (void)hipHostFree(c->pinned_small);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* hbam_last_error(const hbam_ctx* c) { return c ? c->err.c_str() : "null context"; }
+void* hbam_stream(hbam_ctx* c) { return c ? (void*)c->stream : nullptr; }
+int hbam_get_timing(const hbam_ctx* c, hbam_timing* out) {
+  if (!c || !out) return HBAM_EINVAL;
+  *out = c->timing;
+  return HBAM_OK;
+}
+
+int hbam_upload(hbam_ctx* c, const uint8_t* host, uint64_t len, uint8_t** dev_out) {
+  if (!c || !dev_out) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  uint8_t* d = nullptr;
+  HIPCHK(c, hipMalloc(&d, len + 64));
+  HIPCHK(c, hipMemsetAsync(d + len, 0, 64, c->stream));
+  if (len) HIPCHK(c, hipMemcpyAsync(d, host, len, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *dev_out = d;
+  return HBAM_OK;
+}
+
+int hbam_device_free(hbam_ctx* c, uint8_t* dev) {
+  if (!c) return HBAM_EINVAL;
+  if (dev) HIPCHK(c, hipFree(dev));
+  return HBAM_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Stage host bytes in the context's comp buffer (device, padded); return device ptr.
+int stage_comp(hbam_ctx* c, const uint8_t* comp, int on_device, uint64_t len, const uint8_t** d) {
+  if (on_device) {
+    *d = comp;
+    return HBAM_OK;
+  }
+  uint8_t* dc;
+  int rc = ensure(c, B_COMP, len + 64, &dc);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(dc + len, 0, 64, c->stream));
+  if (len) HIPCHK(c, hipMemcpyAsync(dc, comp, len, hipMemcpyHostToDevice, c->stream));
+  *d = dc;
+  return HBAM_OK;
+}
+
+// host-side BAM header parse over inflated bytes (SAMHeaderReader / [htsjdk] BAMFileReader)
+int parse_header_bytes(const uint8_t* u, uint64_t n, hbam_header* h, bool* need_more) {
+  *need_more = false;
+  auto need = [&](uint64_t k) { return k > n; };
+  if (need(8)) { *need_more = true; return HBAM_OK; }
+  if (memcmp(u, "BAM\1", 4) != 0) return HBAM_EFORMAT;
+  const int32_t l_text = rd32(u + 4);
+  if (l_text < 0) return HBAM_EFORMAT;
+  uint64_t p = 8 + (uint64_t)l_text;
+  if (need(p + 4)) { *need_more = true; return HBAM_OK; }
+  int32_t sq = 0;
+  for (int32_t i = 0; i + 3 < l_text; ++i)
+    if ((i == 0 || u[8 + i - 1] == '\n') && u[8 + i] == '@' && u[8 + i + 1] == 'S' && u[8 + i + 2] == 'Q')
+      ++sq;
+  const int32_t n_ref = rd32(u + p);
+  if (n_ref < 0) return HBAM_EFORMAT;
+  p += 4;
+  for (int32_t i = 0; i < n_ref; ++i) {
+    if (need(p + 4)) { *need_more = true; return HBAM_OK; }
+    const int32_t ln = rd32(u + p);
+    if (ln <= 0) return HBAM_EFORMAT;
+    p += 4 + (uint64_t)ln + 4;
+    if (need(p)) { *need_more = true; return HBAM_OK; }
+  }
+  if (sq > 0 && sq != n_ref) return HBAM_EFORMAT;
+  h->l_text = l_text;
+  h->n_ref = n_ref;
+  h->header_ulen = p;
+  return HBAM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hbam_parse_header(hbam_ctx* c, const uint8_t* file, int on_device, uint64_t len,
+                      hbam_header* out) {
+  if (!c || !file || !out) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint8_t* d;
+  int rc = stage_comp(c, file, on_device, len, &d);
+  if (rc) return rc;
+  Chain ch;
+  if ((rc = build_chain(c, d, len, 0, true, &ch))) return rc;
+  if (ch.nb == 0) return set_err(c, ch.end_code == HBAM_EEOF ? HBAM_EFORMAT : ch.end_code,
+                                 "no BGZF block at offset 0");
+  // inflate a growing prefix of blocks until the header parses
+  BlockRec* blk = (BlockRec*)c->bufs[B_BLK].p;
+  uint64_t take = std::min<uint64_t>(ch.nb, 4);
+  for (;;) {
+    std::vector<BlockRec> hb(take);
+    HIPCHK(c, copy_sync(c, hb.data(), blk, take * sizeof(BlockRec), hipMemcpyDeviceToHost));
+    std::vector<uint64_t> uo(take + 1, 0);
+    for (uint64_t i = 0; i < take; ++i) uo[i + 1] = uo[i] + std::min<uint32_t>(hb[i].isize, 65536u);
+    uint64_t *duoff;
+    uint8_t* ub;
+    int32_t* st;
+    if ((rc = ensure(c, B_UOFF, take + 1, &duoff))) return rc;
+    if ((rc = ensure(c, B_UBUF, uo[take] + 64, &ub))) return rc;
+    if ((rc = ensure(c, B_INFST, take, &st))) return rc;
+    HIPCHK(c, hipMemcpyAsync(duoff, uo.data(), (take + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if ((rc = inflate_blocks(c, d, blk, take, duoff, ub, st, false, nullptr))) return rc;
+    std::vector<int32_t> hst(take);
+    std::vector<uint8_t> hu(uo[take] + 1);
+    HIPCHK(c, hipMemcpyAsync(hst.data(), st, take * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(hu.data(), ub, uo[take], hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint64_t good = uo[take];
+    for (uint64_t i = 0; i < take; ++i)
+      if (hst[i] != INF_OK || hb[i].isize > 65536u) { good = uo[i]; break; }
+    bool more = false;
+    rc = parse_header_bytes(hu.data(), good, out, &more);
+    if (rc) return set_err(c, rc, "invalid BAM header");
+    if (!more) {
+      // first voffset: normalized pointer after the header
+      uint64_t p = out->header_ulen;
+      uint64_t i = 0;
+      while (i < take && uo[i + 1] <= p) ++i;
+      if (i == take) {
+        out->first_voffset = (hb[take - 1].coff + hb[take - 1].clen) << 16;
+      } else {
+        out->first_voffset = hb[i].coff << 16 | (p - uo[i]);
+      }
+      return HBAM_OK;
+    }
+    if (good < uo[take] || take == ch.nb)
+      return set_err(c, HBAM_EFORMAT, "truncated BAM header");
+    take = std::min<uint64_t>(ch.nb, take * 2);
+  }
+}
+
+int hbam_scan_blocks(hbam_ctx* c, const uint8_t* comp, int on_device, uint64_t len,
+                     uint64_t base_off, hbam_block* out, uint64_t cap, uint64_t* n_out) {
+  if (!c || !comp || !n_out) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint8_t* d;
+  int rc = stage_comp(c, comp, on_device, len, &d);
+  if (rc) return rc;
+  Chain ch;
+  if ((rc = build_chain(c, d, len, 0, true, &ch))) return rc;
+  *n_out = ch.nb;
+  if (out && ch.nb) {
+    std::vector<BlockRec> hb(ch.nb);
+    HIPCHK(c, copy_sync(c, hb.data(), c->bufs[B_BLK].p, ch.nb * sizeof(BlockRec),
+                        hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < ch.nb && i < cap; ++i) {
+      out[i].coff = hb[i].coff + base_off;
+      out[i].clen = hb[i].clen;
+      out[i].isize = hb[i].isize;
+      out[i].crc = hb[i].crc;
+      out[i].pad = 0;
+    }
+  }
+  return ch.end_code == HBAM_EEOF ? HBAM_OK : set_err(c, ch.end_code, "BGZF chain ends at %llu",
+                                                      (unsigned long long)ch.end_pos);
+}
+
+int hbam_inflate(hbam_ctx* c, const uint8_t* comp, int on_device, uint64_t comp_len,
+                 const hbam_block* blks, uint64_t n, int check_crc, uint8_t* out, uint64_t out_cap,
+                 uint64_t* out_off, int32_t* blk_status) {
+  if (!c || !comp || (!blks && n)) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint8_t* d;
+  int rc = stage_comp(c, comp, on_device, comp_len, &d);
+  if (rc) return rc;
+  std::vector<BlockRec> hb(n);
+  std::vector<uint64_t> uo(n + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (blks[i].coff + blks[i].clen > comp_len || blks[i].clen < 18)
+      return set_err(c, HBAM_EINVAL, "block %llu outside the buffer", (unsigned long long)i);
+    hb[i].coff = blks[i].coff;
+    hb[i].clen = blks[i].clen;
+    hb[i].isize = blks[i].isize;
+    hb[i].crc = blks[i].crc;
+    hb[i].pad = 0;
+    if (blks[i].isize > 65536u)
+      return set_err(c, HBAM_EUNSUPPORTED, "ISIZE > 65536 in block %llu", (unsigned long long)i);
+    uo[i + 1] = uo[i] + blks[i].isize;
+  }
+  if (out_off) memcpy(out_off, uo.data(), (n + 1) * 8);
+  if (out && uo[n] > out_cap) return set_err(c, HBAM_EINVAL, "output buffer too small");
+  BlockRec* db;
+  uint64_t* duoff;
+  uint8_t* ub;
+  int32_t* st;
+  uint32_t* crc;
+  if ((rc = ensure(c, B_BLK, n + 1, &db))) return rc;
+  if ((rc = ensure(c, B_UOFF, n + 1, &duoff))) return rc;
+  if ((rc = ensure(c, B_UBUF, uo[n] + 64, &ub))) return rc;
+  if ((rc = ensure(c, B_INFST, n + 1, &st))) return rc;
+  if ((rc = ensure(c, B_CRC, n + 1, &crc))) return rc;
+  HIPCHK(c, hipMemcpyAsync(db, hb.data(), n * sizeof(BlockRec), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(duoff, uo.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  if ((rc = inflate_blocks(c, d, db, n, duoff, ub, st, check_crc != 0, crc))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  std::vector<int32_t> hst(n);
+  std::vector<uint32_t> hcrc(n);
+  HIPCHK(c, hipMemcpyAsync(hst.data(), st, n * 4, hipMemcpyDeviceToHost, c->stream));
+  if (check_crc) HIPCHK(c, hipMemcpyAsync(hcrc.data(), crc, n * 4, hipMemcpyDeviceToHost, c->stream));
+  if (out && uo[n]) HIPCHK(c, hipMemcpyAsync(out, ub, uo[n], hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
+  c->timing = hbam_timing{};
+  c->timing.inflate_ms = ms;
+  c->timing.n_blocks = n;
+  c->timing.ubuf_bytes = uo[n];
+  for (uint64_t i = 0; i < n; ++i) {
+    int32_t s = hst[i] == INF_OK ? HBAM_OK : hst[i] == INF_SHORT ? HBAM_EFORMAT : HBAM_EDATA;
+    if (s == HBAM_OK && check_crc && hcrc[i] != hb[i].crc) s = HBAM_EFORMAT;
+    if (blk_status) blk_status[i] = s;
+  }
+  return HBAM_OK;
+}
+
+}  // extern "C"
+
+// =====================================================================================
+// hbam_decode_split
+// =====================================================================================
+namespace {
+
+int fill_columns(hbam_ctx* c, uint64_t n, DevColumns* dc) {
+  int rc;
+#define E(id, field, T)                                            \
+  if ((rc = ensure(c, id, n + 1, (T**)&dc->field))) return rc;
+  E(B_C_STATUS, status, int32_t)
+  E(B_C_BS, block_size, int32_t)
+  E(B_C_REF, ref_id, int32_t)
+  E(B_C_POS, pos, int32_t)
+  E(B_C_LRN, l_read_name, uint8_t)
+  E(B_C_MAPQ, mapq, uint8_t)
+  E(B_C_BIN, bin, uint16_t)
+  E(B_C_NCIG, n_cigar, uint16_t)
+  E(B_C_FLAG, flag, uint16_t)
+  E(B_C_LSEQ, l_seq, int32_t)
+  E(B_C_NREF, next_ref_id, int32_t)
+  E(B_C_NPOS, next_pos, int32_t)
+  E(B_C_TLEN, tlen, int32_t)
+  E(B_C_KEY, key, int64_t)
+  E(B_C_LAYOUT, layout_ok, uint8_t)
+  E(B_C_NAMELEN, name_len, uint32_t)
+  E(B_C_CIGN, cigar_n, uint32_t)
+  E(B_C_SEQLEN, seq_len, uint32_t)
+  E(B_C_AUXLEN, aux_len, uint32_t)
+  E(B_C_NAMEOFF, name_off, uint64_t)
+  E(B_C_CIGOFF, cigar_off, uint64_t)
+  E(B_C_SEQOFF, seq_off, uint64_t)
+  E(B_C_AUXOFF, aux_off, uint64_t)
+#undef E
+  return HBAM_OK;
+}
+
+float ev_ms(hbam_ctx* c, int a, int b) {
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev[a], c->ev[b]);
+  return ms;
+}
+
+}  // namespace
+
+extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device,
+                                 uint64_t comp_base, uint64_t comp_len, uint64_t file_len,
+                                 uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                                 hbam_columns* out) {
+  if (!c || !comp || !out) return HBAM_EINVAL;
+  memset(out, 0, sizeof *out);
+  HIPCHK(c, hipSetDevice(c->device));
+  c->timing = hbam_timing{};
+  const uint8_t* d;
+  int rc = stage_comp(c, comp, on_device, comp_len, &d);
+  if (rc) return rc;
+  if (n_ref < 0) {
+    if (comp_base != 0) return set_err(c, HBAM_EINVAL, "n_ref < 0 needs the file start");
+    hbam_header h;
+    if ((rc = hbam_parse_header(c, d, 1, comp_len, &h))) {
+      out->status = rc;
+      return rc;
+    }
+    n_ref = h.n_ref;
+  }
+  const uint64_t coff_s = v_start >> 16;
+  const uint32_t uoff_s = (uint32_t)(v_start & 0xffff);
+  if (coff_s < comp_base || coff_s > comp_base + comp_len)
+    return set_err(c, HBAM_EINVAL, "v_start outside the compressed window");
+  const uint64_t start = coff_s - comp_base;
+  const bool window_is_file_end = (comp_base + comp_len >= file_len);
+
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  Chain ch;
+  if ((rc = build_chain(c, d, comp_len, start, window_is_file_end, &ch))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  BlockRec* blk = (BlockRec*)c->bufs[B_BLK].p;
+  uint64_t nb = ch.nb;
+
+  // ---- BCIS.seek(vStart): first block (empty -> the following one), offset checks
+  if (nb == 0) {
+    // readBlock at vStart's block fails (or EOF: count == 0 -> empty current block)
+    if (ch.end_code == HBAM_EEOF) {
+      // seek to a position at/after the end: empty block, offset must be 0 and eof
+      if (uoff_s != 0) { out->status = HBAM_EIO; return HBAM_OK; }
+      out->status = HBAM_OK;
+      return HBAM_OK;
+    }
+    out->status = ch.end_code == HBAM_ERUNTIMEIO ? HBAM_EIO : ch.end_code;
+    return HBAM_OK;
+  }
+  // blocks: table is device resident; ISIZE clamp + first oversized block
+  uint32_t* isz;
+  uint64_t* uoff;
+  uint64_t* small;
+  if ((rc = ensure(c, B_ISZ32, nb + 1, &isz))) return rc;
+  if ((rc = ensure(c, B_UOFF, nb + 1, &uoff))) return rc;
+  if ((rc = ensure(c, B_SMALL, 16, &small))) return rc;
+  HIPCHK(c, hipMemsetAsync(small, 0xff, 8 * 8, c->stream));
+  HIPCHK(c, hipMemsetAsync(small + 8, 0, 8 * 8, c->stream));
+  k_isize32<<<grid_for(nb, 256), 256, 0, c->stream>>>(blk, nb, isz, (uint32_t*)small);
+  uint64_t utotal = 0;
+  if ((rc = scan_exclusive<uint32_t>(c, isz, nb, uoff, &utotal))) return rc;
+  // first blocks (host view) for the seek semantics
+  BlockRec b0[2];
+  HIPCHK(c, copy_sync(c, b0, blk, std::min<uint64_t>(nb, 2) * sizeof(BlockRec), hipMemcpyDeviceToHost));
+  uint32_t big_first;
+  HIPCHK(c, copy_sync(c, &big_first, small, 4, hipMemcpyDeviceToHost));
+  // inflate
+  uint8_t* ub;
+  int32_t* st;
+  uint32_t* crc;
+  if ((rc = ensure(c, B_UBUF, utotal + 64, &ub))) return rc;
+  if ((rc = ensure(c, B_INFST, nb + 1, &st))) return rc;
+  if ((rc = ensure(c, B_CRC, nb + 1, &crc))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  if ((rc = inflate_blocks(c, d, blk, nb, uoff, ub, st, c->opts.check_crc != 0, crc))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  unsigned long long* first_bad = (unsigned long long*)small + 1;
+  k_first_bad_block<<<grid_for(nb, 256), 256, 0, c->stream>>>(st, crc, blk, nb, c->opts.check_crc,
+                                                             first_bad);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small, small, 16, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  uint64_t fb = c->pinned_small[1];
+  const uint32_t bigi = (uint32_t)(c->pinned_small[0] & 0xffffffffu);
+  int32_t fb_code = HBAM_EEOF;
+  if (fb != ~0ULL) {
+    int32_t s;
+    HIPCHK(c, copy_sync(c, &s, st + fb, 4, hipMemcpyDeviceToHost));
+    fb_code = (s == INF_DATA) ? HBAM_EDATA : HBAM_EFORMAT;
+  }
+  if (bigi != 0xffffffffu && (fb == ~0ULL || bigi < fb)) {
+    fb = bigi;
+    fb_code = HBAM_EUNSUPPORTED;
+  }
+  (void)big_first;
+  // hard end: first failing block, else the chain end
+  uint64_t hard_end;
+  int32_t hard_code;
+  if (fb != ~0ULL) {
+    HIPCHK(c, copy_sync(c, &hard_end, uoff + fb, 8, hipMemcpyDeviceToHost));
+    hard_code = fb_code;
+  } else {
+    hard_end = utotal;
+    hard_code = ch.end_code;
+  }
+  // seek: block 0 (or 1 if block 0 is empty)
+  uint64_t sblk = 0;
+  if (b0[0].isize == 0) {
+    if (fb == 0) { out->status = fb_code; return HBAM_OK; }
+    sblk = 1;
+  }
+  if (fb == sblk) { out->status = fb_code; return HBAM_OK; }
+  uint64_t r0;
+  if (sblk >= nb) {
+    // available() after an empty last block: EOF or readBlock error
+    if (ch.end_code != HBAM_EEOF) { out->status = ch.end_code == HBAM_ERUNTIMEIO ? HBAM_EIO : ch.end_code; return HBAM_OK; }
+    if (uoff_s != 0) { out->status = HBAM_EIO; return HBAM_OK; }
+    out->status = HBAM_OK;
+    return HBAM_OK;
+  }
+  {
+    const BlockRec& bs = b0[sblk];
+    const uint64_t after = comp_base + bs.coff + bs.clen;  // file position after the block
+    const bool eof = (after == file_len) || (file_len - after == 28);
+    if (uoff_s > bs.isize || (uoff_s == bs.isize && !eof)) { out->status = HBAM_EIO; return HBAM_OK; }
+    uint64_t u0;
+    HIPCHK(c, copy_sync(c, &u0, uoff + sblk, 8, hipMemcpyDeviceToHost));
+    r0 = u0 + uoff_s;
+  }
+  // events: empty blocks after the seek block, at positions <= hard_end
+  uint64_t* evd;
+  if ((rc = ensure(c, B_EVENTS, 1024, &evd))) return rc;
+  uint32_t* nev_d = (uint32_t*)(small + 4);
+  HIPCHK(c, hipMemsetAsync(nev_d, 0, 4, c->stream));
+  if (nb > sblk + 1)
+    k_collect_empty<<<grid_for(nb - sblk - 1, 256), 256, 0, c->stream>>>(blk + sblk, uoff + sblk,
+                                                                         nb - sblk, evd, nev_d, 1024);
+  uint32_t nev = 0;
+  HIPCHK(c, hipMemcpyAsync(&nev, nev_d, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (nev > 1024) return set_err(c, HBAM_EUNSUPPORTED, "more than 1024 empty BGZF blocks in a split");
+  // events beyond the hard end cannot be reached; keep them (empty_at checks <= hard_end)
+
+  // ---- K5: record starts (blocks [sblk, nb))
+  const uint64_t wb = nb - sblk;
+  const uint64_t* uo = uoff + sblk;
+  uint64_t *entry, *exitp, *rbase, *rec_off, *voff;
+  uint16_t* rel;
+  uint32_t *count, *badlist;
+  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  if ((rc = ensure(c, B_ENTRY, wb + 1, &entry))) return rc;
+  if ((rc = ensure(c, B_EXIT, wb + 1, &exitp))) return rc;
+  if ((rc = ensure(c, B_REL, wb * WALK_CAP, &rel))) return rc;
+  if ((rc = ensure(c, B_COUNT, wb + 1, &count))) return rc;
+  if ((rc = ensure(c, B_RECBASE, wb + 1, &rbase))) return rc;
+  if ((rc = ensure(c, B_BADLIST, wb + 1, &badlist))) return rc;
+  if (wb > 1)
+    k_block_entry<<<(uint32_t)(wb - 1), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, n_ref,
+                                                            entry);
+  k_block_walk<<<grid_for(wb, 64), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, r0, hard_end, entry, rel,
+                                                       count, exitp);
+  uint32_t* nbad_d = (uint32_t*)(small + 5);
+  HIPCHK(c, hipMemsetAsync(nbad_d, 0, 4, c->stream));
+  if (wb > 1)
+    k_stitch_check<<<grid_for(wb - 1, 256), 256, 0, c->stream>>>(entry, exitp, (uint32_t)wb, nbad_d,
+                                                                 badlist, (uint32_t)wb);
+  uint32_t nbad = 0;
+  HIPCHK(c, hipMemcpyAsync(&nbad, nbad_d, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (nbad) {
+    // sort the mismatch list (atomic order is arbitrary)
+    std::vector<uint32_t> bl(nbad);
+    HIPCHK(c, copy_sync(c, bl.data(), badlist, nbad * 4, hipMemcpyDeviceToHost));
+    std::sort(bl.begin(), bl.end());
+    HIPCHK(c, copy_sync(c, badlist, bl.data(), nbad * 4, hipMemcpyHostToDevice));
+    k_chain_fix<<<1, 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, entry, rel, count, exitp,
+                                         badlist, nbad);
+    HIPCHK(c, hipGetLastError());
+  }
+  uint64_t nrec = 0;
+  if ((rc = scan_exclusive<uint32_t>(c, count, wb, rbase, &nrec))) return rc;
+  if ((rc = ensure(c, B_RECOFF, nrec + 1, &rec_off))) return rc;
+  if ((rc = ensure(c, B_VOFF, nrec + 1, &voff))) return rc;
+  k_emit_offsets<<<(uint32_t)wb, 256, 0, c->stream>>>(uo, blk + sblk, (uint32_t)wb, rel, count, rbase,
+                                                      rec_off, voff);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
+
+  // ---- K6/K7/K8
+  DevColumns dc{};
+  if ((rc = fill_columns(c, nrec, &dc))) return rc;
+  unsigned long long* first_stop = (unsigned long long*)small + 6;
+  HIPCHK(c, hipMemsetAsync(first_stop, 0xff, 8, c->stream));
+  if (nrec)
+    k_decode_fixed<<<grid_for(nrec, 256), 256, 0, c->stream>>>(
+        ub, nrec, rec_off, voff, v_end, hard_end, hard_code, evd, nev, n_ref, c->opts.validate_refs,
+        dc, first_stop);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev[6], c->stream));
+  uint64_t fs;
+  HIPCHK(c, hipMemcpyAsync(&fs, first_stop, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  uint64_t n_final = std::min<uint64_t>(fs, nrec);
+  int32_t status = HBAM_OK;
+  uint64_t err_rec = 0;
+  if (fs < nrec) {
+    int32_t s;
+    HIPCHK(c, copy_sync(c, &s, dc.status + fs, 4, hipMemcpyDeviceToHost));
+    if (s < 0) {
+      status = s;
+      err_rec = fs;
+    }
+  } else if (nrec > 0 || hard_code != HBAM_EEOF) {
+    // chain ended without a stop record: the walker stopped at a CHAIN_STOP
+  }
+  // ---- pools
+  uint64_t tot_name = 0, tot_cig = 0, tot_seq = 0, tot_aux = 0;
+  if ((rc = scan_exclusive<uint32_t>(c, dc.name_len, n_final, dc.name_off, &tot_name))) return rc;
+  if ((rc = scan_exclusive<uint32_t>(c, dc.cigar_n, n_final, dc.cigar_off, &tot_cig))) return rc;
+  if ((rc = scan_exclusive<uint32_t>(c, dc.seq_len, n_final, dc.seq_off, &tot_seq))) return rc;
+  if ((rc = scan_exclusive<uint32_t>(c, dc.aux_len, n_final, dc.aux_off, &tot_aux))) return rc;
+  if ((rc = ensure(c, B_C_NAMES, tot_name + 1, &dc.names))) return rc;
+  if ((rc = ensure(c, B_C_CIGARS, tot_cig + 1, &dc.cigars))) return rc;
+  if ((rc = ensure(c, B_C_SEQ, tot_seq + 1, &dc.seq))) return rc;
+  if ((rc = ensure(c, B_C_QUAL, tot_seq + 1, &dc.qual))) return rc;
+  if ((rc = ensure(c, B_C_AUX, tot_aux + 1, &dc.aux))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+  if (n_final)
+    k_decode_pools<<<grid_for(n_final, 4), 256, 0, c->stream>>>(ub, n_final, rec_off, dc);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+
+  out->n_records = n_final;
+  out->status = status;
+  out->err_record = err_rec;
+  out->voffset = voff;
+  out->key = dc.key;
+  out->rec_off = rec_off;
+  out->ubuf = ub;
+  out->ubuf_len = utotal;
+  out->block_size = dc.block_size;
+  out->ref_id = dc.ref_id;
+  out->pos = dc.pos;
+  out->l_read_name = dc.l_read_name;
+  out->mapq = dc.mapq;
+  out->bin = dc.bin;
+  out->n_cigar = dc.n_cigar;
+  out->flag = dc.flag;
+  out->l_seq = dc.l_seq;
+  out->next_ref_id = dc.next_ref_id;
+  out->next_pos = dc.next_pos;
+  out->tlen = dc.tlen;
+  out->layout_ok = dc.layout_ok;
+  out->name_off = dc.name_off;
+  out->names = dc.names;
+  out->cigar_off = dc.cigar_off;
+  out->cigars = dc.cigars;
+  out->seq_off = dc.seq_off;
+  out->seq = dc.seq;
+  out->qual = dc.qual;
+  out->aux_off = dc.aux_off;
+  out->aux = dc.aux;
+
+  c->timing.scan_ms = ev_ms(c, 0, 1);
+  c->timing.inflate_ms = ev_ms(c, 2, 3);
+  c->timing.walk_ms = ev_ms(c, 4, 5);
+  c->timing.decode_ms = ev_ms(c, 5, 6);
+  c->timing.pools_ms = ev_ms(c, 7, 8);
+  c->timing.total_ms = ev_ms(c, 0, 8);
+  c->timing.n_blocks = nb;
+  c->timing.comp_bytes = ch.end_pos - start;
+  c->timing.ubuf_bytes = utotal;
+  c->timing.n_records = n_final;
+  c->timing.pool_bytes = tot_name + 4 * tot_cig + 2 * tot_seq + tot_aux;
+  return HBAM_OK;
+}
+
+extern "C" int hbam_columns_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_columns* h) {
+  if (!c || !dv || !h) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  memset(h, 0, sizeof *h);
+  const uint64_t n = dv->n_records;
+  h->n_records = n;
+  h->status = dv->status;
+  h->err_record = dv->err_record;
+  h->ubuf_len = dv->ubuf_len;
+  auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
+    if (!bytes) return HBAM_OK;
+    if (!src) return HBAM_EINVAL;
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    return HBAM_OK;
+  };
+#define ALLOC(field, T, cnt)                                          \
+  h->field = (T*)malloc(sizeof(T) * ((cnt) ? (cnt) : 1));              \
+  if (!h->field) return HBAM_ENOMEM;                                  \
+  if ((rc = cp(h->field, dv->field, sizeof(T) * (cnt)))) return rc;
+  int rc;
+  ALLOC(voffset, uint64_t, n)
+  ALLOC(key, int64_t, n)
+  ALLOC(rec_off, uint64_t, n)
+  ALLOC(block_size, int32_t, n)
+  ALLOC(ref_id, int32_t, n)
+  ALLOC(pos, int32_t, n)
+  ALLOC(l_read_name, uint8_t, n)
+  ALLOC(mapq, uint8_t, n)
+  ALLOC(bin, uint16_t, n)
+  ALLOC(n_cigar, uint16_t, n)
+  ALLOC(flag, uint16_t, n)
+  ALLOC(l_seq, int32_t, n)
+  ALLOC(next_ref_id, int32_t, n)
+  ALLOC(next_pos, int32_t, n)
+  ALLOC(tlen, int32_t, n)
+  ALLOC(layout_ok, uint8_t, n)
+  ALLOC(name_off, uint64_t, n + 1)
+  ALLOC(cigar_off, uint64_t, n + 1)
+  ALLOC(seq_off, uint64_t, n + 1)
+  ALLOC(aux_off, uint64_t, n + 1)
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t nn = n ? h->name_off[n] : 0, nc = n ? h->cigar_off[n] : 0,
+                 ns = n ? h->seq_off[n] : 0, na = n ? h->aux_off[n] : 0;
+  ALLOC(names, uint8_t, nn)
+  ALLOC(cigars, uint32_t, nc)
+  ALLOC(seq, uint8_t, ns)
+  ALLOC(qual, uint8_t, ns)
+  ALLOC(aux, uint8_t, na)
+#undef ALLOC
+  h->ubuf = nullptr;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBAM_OK;
+}
+
+extern "C" void hbam_free_host_columns(hbam_columns* h) {
+  if (!h) return;
+  void* ps[] = {h->voffset, h->key, h->rec_off, h->block_size, h->ref_id, h->pos, h->l_read_name,
+                h->mapq, h->bin, h->n_cigar, h->flag, h->l_seq, h->next_ref_id, h->next_pos, h->tlen,
+                h->layout_ok, h->name_off, h->cigar_off, h->seq_off, h->aux_off, h->names, h->cigars,
+                h->seq, h->qual, h->aux};
+  for (void* p : ps) free(p);
+  memset(h, 0, sizeof *h);
+}
+
+extern "C" void hbam_release_columns(hbam_ctx* c, hbam_columns* dv) {
+  (void)c;
+  if (dv) memset(dv, 0, sizeof *dv);
+}
+
+// =====================================================================================
+// Guessers (kernels in hbam_guess.hip)
+// =====================================================================================
+namespace {
+struct GuessWork {
+  uint8_t* scratch;
+  uint8_t* lens;
+  uint8_t* bufs;
+  int64_t *beg, *end, *out;
+  int32_t* err;
+};
+int guess_work(hbam_ctx* c, uint64_t k, GuessWork* w) {
+  // carve from B_REL / B_LENS / B_PARTIAL-like dedicated slots: use B_UBUF for scratch
+  int rc;
+  uint8_t* base;
+  const uint64_t per = 65536 + LENS_SLOT + 8 + 8 * 3 + 4;
+  if ((rc = ensure(c, B_UBUF, k * per + 4096, &base))) return rc;
+  w->scratch = base;
+  w->lens = base + k * 65536;
+  w->bufs = w->lens + k * LENS_SLOT;
+  uint8_t* q = w->bufs + k * 8;
+  q = (uint8_t*)(((uintptr_t)q + 15) & ~(uintptr_t)15);
+  w->beg = (int64_t*)q;
+  w->end = w->beg + k;
+  w->out = w->end + k;
+  w->err = (int32_t*)(w->out + k);
+  return HBAM_OK;
+}
+}  // namespace
+
+extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device, uint64_t file_len,
+                                const int64_t* beg, const int64_t* end, uint64_t k, int32_t n_ref,
+                                int64_t* out, int32_t* err) {
+  if (!c || !file || (k && (!beg || !end || !out || !err))) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (k == 0) return HBAM_OK;
+  const uint8_t* d;
+  int rc = stage_comp(c, file, on_device, file_len, &d);
+  if (rc) return rc;
+  GuessWork w;
+  if ((rc = guess_work(c, k, &w))) return rc;
+  // Initial ByteBuffer of BAMSplitGuesser(ss, conf): the ctor reads the file magic into it
+  // (:85-87).  Only windows shorter than 4 bytes could observe a stale buffer carried over
+  // from a previous guess, and those always return `end` (the XLEN seek at p0+10 fails),
+  // so guesses are independent.
+  uint8_t magic[8] = {0};
+  {
+    const uint64_t n4 = std::min<uint64_t>(file_len, 4);
+    if (n4) {
+      HIPCHK(c, hipMemcpyAsync(c->pinned_small, d, n4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      memcpy(magic, c->pinned_small, n4);
+    }
+  }
+  std::vector<uint8_t> ib(k * 8);
+  for (uint64_t i = 0; i < k; ++i) memcpy(&ib[i * 8], magic, 8);
+  HIPCHK(c, hipMemcpyAsync(w.bufs, ib.data(), k * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(w.beg, beg, k * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(w.end, end, k * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[9], c->stream));
+  k_guess_bam<<<grid_for(k, GUESS_WG), GUESS_WG, 0, c->stream>>>(d, (int64_t)file_len, w.beg, w.end,
+                                                                (uint32_t)k, n_ref, w.scratch, w.lens,
+                                                                w.bufs, w.out, w.err);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev[10], c->stream));
+  HIPCHK(c, hipMemcpyAsync(out, w.out, k * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(err, w.err, k * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->timing = hbam_timing{};
+  c->timing.total_ms = ev_ms(c, 9, 10);
+  return HBAM_OK;
+}
+
+extern "C" int64_t hbam_guess_bam_record_start(hbam_ctx* c, const uint8_t* file, int on_device,
+                                               uint64_t file_len, int64_t beg, int64_t end,
+                                               int32_t n_ref, int32_t* err) {
+  int64_t out = end;
+  int32_t e = HBAM_OK;
+  const int rc = hbam_guess_batch(c, file, on_device, file_len, &beg, &end, 1, n_ref, &out, &e);
+  if (err) *err = rc ? rc : e;
+  return out;
+}
+
+extern "C" int64_t hbam_guess_bgzf_block_start(hbam_ctx* c, const uint8_t* file, int on_device,
+                                               uint64_t file_len, int64_t beg, int64_t end,
+                                               int32_t* err) {
+  if (!c || !file) {
+    if (err) *err = HBAM_EINVAL;
+    return end;
+  }
+  if (hipSetDevice(c->device) != hipSuccess) {
+    if (err) *err = HBAM_EDEVICE;
+    return end;
+  }
+  const uint8_t* d;
+  int rc = stage_comp(c, file, on_device, file_len, &d);
+  GuessWork w;
+  if (!rc) rc = guess_work(c, 1, &w);
+  if (rc) {
+    if (err) *err = rc;
+    return end;
+  }
+  int64_t out = end;
+  int32_t e = HBAM_OK;
+  if (hipMemcpyAsync(w.beg, &beg, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(w.end, &end, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    if (err) *err = HBAM_EDEVICE;
+    return end;
+  }
+  k_guess_bgzf<<<1, GUESS_WG, 0, c->stream>>>(d, (int64_t)file_len, w.beg, w.end, 1, w.scratch,
+                                              w.lens, w.out, w.err);
+  if (hipMemcpyAsync(&out, w.out, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipMemcpyAsync(&e, w.err, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    if (err) *err = HBAM_EDEVICE;
+    return end;
+  }
+  if (err) *err = e;
+  return out;
+}
+
+// BAMInputFormat.addProbabilisticSplits (BAMInputFormat.java:163-224) for one file.
+extern "C" int64_t hbam_probabilistic_splits(hbam_ctx* c, const uint8_t* file, int on_device,
+                                             uint64_t file_len, const uint64_t* beg,
+                                             const uint64_t* end, uint64_t n, uint64_t* v_start,
+                                             uint64_t* v_end) {
+  if (!c || !file || (n && (!beg || !end || !v_start || !v_end))) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint8_t* d;
+  int rc = stage_comp(c, file, on_device, file_len, &d);
+  if (rc) return rc;
+  hbam_header h;
+  if ((rc = hbam_parse_header(c, d, 1, file_len, &h))) return rc;  // BAMSplitGuesser ctor
+  uint8_t m[4] = {0, 0, 0, 0};
+  if (file_len >= 4) {
+    HIPCHK(c, hipMemcpyAsync(c->pinned_small, d, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    memcpy(m, c->pinned_small, 4);
+  }
+  if (file_len < 4 || !(m[0] == 0x1f && m[1] == 0x8b && m[2] == 8 && m[3] == 4))
+    return set_err(c, HBAM_EFORMAT, "Does not seem like a BAM file");
+  std::vector<int64_t> b(n), e(n), g(n);
+  std::vector<int32_t> er(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    b[i] = (int64_t)beg[i];
+    e[i] = (int64_t)end[i];
+  }
+  if ((rc = hbam_guess_batch(c, d, 1, file_len, b.data(), e.data(), n, h.n_ref, g.data(), er.data())))
+    return rc;
+  int64_t out = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (er[i]) return set_err(c, er[i], "guesser raised an exception for split %llu",
+                              (unsigned long long)i);
+    const uint64_t aligned_end = end[i] << 16 | 0xffff;
+    if (g[i] == (int64_t)end[i]) {
+      if (out == 0) return set_err(c, HBAM_EIO, "no reads in first split: bad BAM file or tiny split size?");
+      v_end[out - 1] = aligned_end;
+    } else {
+      v_start[out] = (uint64_t)g[i];
+      v_end[out] = aligned_end;
+      ++out;
+    }
+  }
+  return out;
+}

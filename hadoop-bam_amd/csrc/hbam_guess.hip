@@ -1,0 +1,477 @@
+// hbam_guess.hip — BAMSplitGuesser / BGZFSplitGuesser on the device (gfx950).
+//
+// One lane = one guesser call guessNextBAMRecordStart(beg, end) (BAMSplitGuesser.java:109-212),
+// so BAMInputFormat.addProbabilisticSplits' per-split loop (BAMInputFormat.java:181-222) and
+// config #3's 10k guesses run as one launch.  The lane runs the reference's state machine
+// over the window W = file[beg, beg+min(end-beg, 262139)) with the same cursor semantics the
+// Java code observes:
+//   * SeekableArrayStream (util/SeekableArrayStream.java:29-58) — one shared position used by
+//     both guessNextBGZFPos and the BlockCompressedInputStream, seek bounds, short reads;
+//   * the persistent 8-byte ByteBuffer `buf` (stale bytes survive short reads);
+//   * [htsjdk] BlockCompressedInputStream readBlock/available/read/seek/getFilePointer/eof
+//     with CRC checking on (BAMSplitGuesser.java:130), block cache on seek;
+//   * [htsjdk] BAMRecordCodec.decode with LazyBAMRecordFactory (no refID validation);
+//   * the exception filter of :144-152 and :194-207.
+// Inflate is inflate_dev.h (zlib-exact); CRC32 is computed per inflated block.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hbam_internal.h"
+#include "inflate_dev.h"
+
+namespace hbam {
+
+constexpr int32_t G_MAGIC = 0x04088b1f;
+constexpr int32_t G_MAGIC_SUB = 0x00024342;
+constexpr int32_t G_MAX_BYTES_READ = 3 * 0xffff + 0xfffe;
+constexpr uint32_t GUESS_WG = 64;
+
+struct GStream {  // SeekableArrayStream over the window
+  const uint8_t* a;
+  int64_t len;
+  int64_t pos;
+};
+__device__ __forceinline__ bool gs_seek(GStream& s, int64_t p) {
+  if (p < 0 || p > s.len) return false;  // IOException
+  s.pos = p;
+  return true;
+}
+__device__ __forceinline__ int32_t gs_read(GStream& s, uint8_t* b, int32_t n) {
+  if (s.pos == s.len) return -1;
+  if ((int64_t)n > s.len - s.pos) n = (int32_t)(s.len - s.pos);
+  for (int32_t i = 0; i < n; ++i) b[i] = s.a[s.pos + i];
+  s.pos += n;
+  return n;
+}
+
+struct GBcis {
+  int64_t block_addr;
+  int32_t last_len;
+  int32_t cur_len;  // -1 = mCurrentBlock == null
+  int32_t cur_off;
+  uint8_t* cur;     // 65536-byte global scratch
+  uint16_t* s_ll;
+  uint8_t* s_d;
+  uint8_t* lens;
+  const uint32_t* crc_tab;
+  int check_crc;
+};
+
+__device__ int32_t gb_read_block(GBcis& b, GStream& f) {
+  const int64_t P = f.pos;
+  const int64_t avail = f.len - P;
+  if (avail <= 0) {  // count == 0: no empty gzip block at end
+    b.cur_off = 0;
+    b.block_addr += b.last_len;
+    b.cur_len = 0;
+    return HBAM_OK;
+  }
+  if (avail < 18) { f.pos = f.len; return HBAM_EIO; }  // Premature end of file
+  const uint8_t* h = f.a + P;
+  const int32_t blen = (int32_t)(h[16] | h[17] << 8) + 1;
+  if (blen < 18) { f.pos = P + 18; return HBAM_EIO; }
+  if ((int64_t)blen > avail) { f.pos = f.len; return HBAM_ETRUNC; }
+  f.pos = P + blen;
+  // inflateBlock: mCurrentBlock = null first
+  b.cur_len = -1;
+  const int32_t isize = (int32_t)((uint32_t)h[blen - 4] | (uint32_t)h[blen - 3] << 8 |
+                                  (uint32_t)h[blen - 2] << 16 | (uint32_t)h[blen - 1] << 24);
+  if (isize < 0) return HBAM_ERUNTIMEIO;
+  // BlockGunzipper header checks
+  if (!(h[0] == 0x1f && h[1] == 0x8b && h[2] == 8 && h[3] == 4)) return HBAM_EFORMAT;
+  if ((h[10] | h[11] << 8) != 6) return HBAM_EFORMAT;
+  if (blen < 26) return HBAM_EDATA;
+  if (isize > 65536) return HBAM_EUNSUPPORTED;
+  uint32_t produced = 0;
+  const int32_t st = inflate_raw(h + 18, (uint32_t)(blen - 26), b.cur, (uint32_t)isize, b.s_ll,
+                                 b.s_d, b.lens, &produced);
+  if (st == INF_DATA) return HBAM_EDATA;
+  if (st == INF_SHORT) return HBAM_EFORMAT;
+  if (b.check_crc) {
+    uint32_t c = 0xffffffffu;
+    for (int32_t i = 0; i < isize; ++i) c = b.crc_tab[(c ^ b.cur[i]) & 0xff] ^ (c >> 8);
+    c = ~c;
+    const uint32_t expect = (uint32_t)h[blen - 8] | (uint32_t)h[blen - 7] << 8 |
+                            (uint32_t)h[blen - 6] << 16 | (uint32_t)h[blen - 5] << 24;
+    if (c != expect) return HBAM_EFORMAT;
+  }
+  b.cur_len = isize;
+  b.cur_off = 0;
+  b.block_addr += b.last_len;
+  b.last_len = blen;
+  return HBAM_OK;
+}
+__device__ int32_t gb_available(GBcis& b, GStream& f, int32_t* avail) {
+  if (b.cur_len < 0 || b.cur_off == b.cur_len) {
+    const int32_t rc = gb_read_block(b, f);
+    if (rc) return rc;
+  }
+  *avail = b.cur_len < 0 ? 0 : b.cur_len - b.cur_off;
+  return HBAM_OK;
+}
+// read(): copy into dst (or skip when dst == nullptr); *got = -1 at EOF
+__device__ int32_t gb_read(GBcis& b, GStream& f, uint8_t* dst, int32_t len, int32_t* got) {
+  const int32_t orig = len;
+  int32_t off = 0;
+  while (len > 0) {
+    int32_t av;
+    const int32_t rc = gb_available(b, f, &av);
+    if (rc) return rc;
+    if (av == 0) {
+      if (orig == len) { *got = -1; return HBAM_OK; }
+      break;
+    }
+    const int32_t c = len < av ? len : av;
+    if (dst)
+      for (int32_t i = 0; i < c; ++i) dst[off + i] = b.cur[b.cur_off + i];
+    b.cur_off += c;
+    off += c;
+    len -= c;
+  }
+  *got = orig - len;
+  return HBAM_OK;
+}
+__device__ __forceinline__ bool gb_eof(const GBcis& b, const GStream& f) {
+  if (f.pos == f.len) return true;
+  return f.len - (b.block_addr + b.last_len) == 28;
+}
+__device__ int32_t gb_seek(GBcis& b, GStream& f, uint64_t pos) {
+  const int64_t coff = (int64_t)(pos >> 16);
+  const int32_t uoff = (int32_t)(pos & 0xffff);
+  int32_t avail;
+  if (b.block_addr == coff && b.cur_len >= 0) {
+    avail = b.cur_len;
+  } else {
+    if (!gs_seek(f, coff)) return HBAM_EIO;
+    b.block_addr = coff;
+    b.last_len = 0;
+    int32_t rc = gb_read_block(b, f);
+    if (rc) return rc;
+    rc = gb_available(b, f, &avail);
+    if (rc) return rc;
+  }
+  if (uoff > avail || (uoff == avail && !gb_eof(b, f))) return HBAM_EIO;
+  b.cur_off = uoff;
+  return HBAM_OK;
+}
+__device__ __forceinline__ uint64_t gb_tell(const GBcis& b) {
+  if (b.cur_off == b.cur_len) return (uint64_t)(b.block_addr + b.last_len) << 16;
+  return (uint64_t)b.block_addr << 16 | (uint32_t)b.cur_off;
+}
+// BinaryCodec.readBytes: IOException -> RuntimeIOException, -1 -> RuntimeEOFException
+__device__ int32_t gc_read(GBcis& b, GStream& f, uint8_t* dst, int32_t len) {
+  int32_t total = 0;
+  do {
+    int32_t got;
+    int32_t rc = gb_read(b, f, dst ? dst + total : nullptr, len - total, &got);
+    if (rc == HBAM_EIO) return HBAM_ERUNTIMEIO;
+    if (rc) return rc;
+    if (got < 0) return HBAM_EEOF;
+    total += got;
+  } while (total < len);
+  return HBAM_OK;
+}
+// BAMRecordCodec.decode with the lazy factory: 1 record, 0 null, <0 exception
+__device__ int32_t gc_decode(GBcis& b, GStream& f) {
+  uint8_t t[4];
+  int32_t rc = gc_read(b, f, t, 4);
+  if (rc == HBAM_EEOF) return 0;
+  if (rc) return rc;
+  const int32_t bs = (int32_t)((uint32_t)t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 |
+                               (uint32_t)t[3] << 24);
+  if (bs < 32) return HBAM_EFORMAT;
+  const int32_t fields[11] = {4, 4, 1, 1, 2, 2, 2, 4, 4, 4, 4};
+#pragma unroll
+  for (int k = 0; k < 11; ++k) {
+    rc = gc_read(b, f, nullptr, fields[k]);
+    if (rc) return rc;
+  }
+  if (bs > 32) {
+    rc = gc_read(b, f, nullptr, bs - 32);
+    if (rc) return rc;
+  }
+  return 1;
+}
+
+struct Guesser {
+  GStream in;
+  GBcis bz;
+  uint8_t buf[8];
+  int32_t n_ref;
+};
+__device__ __forceinline__ int32_t gbuf_i32(const Guesser& g, int i) {
+  return (int32_t)((uint32_t)g.buf[i] | (uint32_t)g.buf[i + 1] << 8 | (uint32_t)g.buf[i + 2] << 16 |
+                   (uint32_t)g.buf[i + 3] << 24);
+}
+__device__ __forceinline__ int32_t gbuf_u16(const Guesser& g, int i) {
+  return (int32_t)(g.buf[i] | g.buf[i + 1] << 8);
+}
+
+// guessNextBGZFPos :222-299 (IOException -> null)
+__device__ bool g_next_bgzf(Guesser& g, int32_t p, int32_t end, int32_t* opos, int32_t* osize) {
+  for (;;) {
+    for (;;) {
+      if (!gs_seek(g.in, p)) return false;
+      gs_read(g.in, g.buf, 4);
+      const int32_t n = gbuf_i32(g, 0);
+      if (n == G_MAGIC) break;
+      if ((int32_t)((uint32_t)n >> 8) == 0x00088b1f) ++p;
+      else if ((int32_t)((uint32_t)n >> 16) == 0x00008b1f) p += 2;
+      else p += 3;
+      if (p >= end) return false;
+    }
+    const int32_t p0 = p;
+    p += 10;
+    if (!gs_seek(g.in, p)) return false;
+    gs_read(g.in, g.buf, 2);
+    p += 2;
+    const int32_t xlen = gbuf_u16(g, 0);
+    const int32_t sub_end = p + xlen;
+    bool cancel = false;
+    while (p < sub_end) {
+      gs_read(g.in, g.buf, 4);
+      if (gbuf_i32(g, 0) != G_MAGIC_SUB) {
+        p += 4 + gbuf_u16(g, 2);
+        if (!gs_seek(g.in, p)) return false;
+        continue;
+      }
+      gs_read(g.in, g.buf, 2);
+      const int32_t bsize = gbuf_u16(g, 0);
+      p += 6;
+      while (p < sub_end) {
+        if (!gs_seek(g.in, p)) return false;
+        gs_read(g.in, g.buf, 4);
+        p += 4 + gbuf_u16(g, 2);
+      }
+      if (p != sub_end) { cancel = true; break; }
+      p += bsize - xlen - 19 + 4;
+      if (!gs_seek(g.in, p)) return false;
+      gs_read(g.in, g.buf, 4);
+      *opos = p0;
+      *osize = gbuf_i32(g, 0);
+      return true;
+    }
+    (void)cancel;
+    p = p0 + 4;
+  }
+}
+
+// guessNextBAMPos :301-398
+__device__ int32_t g_next_bam(Guesser& g, uint64_t cpv, int32_t up, int32_t csize) {
+  int32_t got;
+  up += 4;
+  while (up + 35 < csize) {
+    if (gb_seek(g.bz, g.in, cpv | (uint32_t)up)) return -1;
+    if (gb_read(g.bz, g.in, g.buf, 8, &got)) return -1;
+    const int32_t id = gbuf_i32(g, 0), pos = gbuf_i32(g, 4);
+    if (id < -1 || id > g.n_ref || pos < -1) { ++up; continue; }
+    if (gb_seek(g.bz, g.in, cpv | (uint32_t)(up + 20))) return -1;
+    if (gb_read(g.bz, g.in, g.buf, 8, &got)) return -1;
+    const int32_t nid = gbuf_i32(g, 0), npos = gbuf_i32(g, 4);
+    if (nid < -1 || nid > g.n_ref || npos < -1) { ++up; continue; }
+    const int32_t next_up = up + 1;
+    up -= 4;
+    if (gb_seek(g.bz, g.in, cpv | (uint32_t)(up + 12))) return -1;
+    if (gb_read(g.bz, g.in, g.buf, 4, &got)) return -1;
+    const int32_t name_len = gbuf_i32(g, 0) & 0xff;
+    const int32_t nul = up + 36 + name_len - 1;
+    if (nul >= csize) { up = next_up; continue; }
+    if (gb_seek(g.bz, g.in, cpv | (uint32_t)nul)) return -1;
+    if (gb_read(g.bz, g.in, g.buf, 1, &got)) return -1;
+    if (g.buf[0] != 0) { up = next_up; continue; }
+    int32_t zero_min = 32 + name_len;
+    if (gb_seek(g.bz, g.in, cpv | (uint32_t)(up + 16))) return -1;
+    if (gb_read(g.bz, g.in, g.buf, 8, &got)) return -1;
+    zero_min = (int32_t)((uint32_t)zero_min + (uint32_t)(gbuf_i32(g, 0) & 0xffff) * 4u);
+    const int32_t ls = gbuf_i32(g, 4);
+    const int32_t half = (int32_t)((uint32_t)ls + 1u) / 2;
+    zero_min = (int32_t)((uint32_t)zero_min + (uint32_t)ls + (uint32_t)half);
+    if (gb_seek(g.bz, g.in, cpv | (uint32_t)up)) return -1;
+    if (gb_read(g.bz, g.in, g.buf, 4, &got)) return -1;
+    if (gbuf_i32(g, 0) < zero_min) { up = next_up; continue; }
+    return up;
+  }
+  return -1;
+}
+
+// guessNextBAMRecordStart :109-212
+__device__ int64_t g_guess(Guesser& g, const uint8_t* file, int64_t flen, int64_t beg, int64_t end,
+                           int32_t* err) {
+  *err = HBAM_OK;
+  int32_t want = (int32_t)(end - beg);
+  if (want > G_MAX_BYTES_READ) want = G_MAX_BYTES_READ;
+  int64_t total = 0;
+  if (want > 0 && beg >= 0 && beg <= flen) total = (flen - beg < want) ? flen - beg : want;
+  g.in.a = file + ((beg >= 0 && beg <= flen) ? beg : 0);
+  g.in.len = total;
+  g.in.pos = 0;
+  g.bz.block_addr = 0;
+  g.bz.last_len = 0;
+  g.bz.cur_len = -1;
+  g.bz.cur_off = 0;
+  int32_t first_end = (int32_t)(end - beg);
+  if (first_end > 0xffff) first_end = 0xffff;
+  for (int32_t cp = 0;; ++cp) {
+    int32_t ppos, psize;
+    if (!g_next_bgzf(g, cp, first_end, &ppos, &psize)) return end;
+    const int32_t cp0 = cp = ppos;
+    const uint64_t cpv = (uint64_t)(uint32_t)cp0 << 16;
+    if (gb_seek(g.bz, g.in, cpv)) continue;  // catch (Throwable)
+    for (int32_t up = 0;; ++up) {
+      const int32_t up0 = up = g_next_bam(g, cpv, up, psize);
+      if (up0 < 0) break;
+      if (gb_seek(g.bz, g.in, cpv | (uint32_t)up0)) { *err = HBAM_EIO; return end; }
+      bool decoded_any = false;
+      int b = 0;
+      int32_t prev = cp0;
+      int32_t rc = 0;
+      while (b < 3) {
+        rc = gc_decode(g.bz, g.in);
+        if (rc <= 0) break;
+        decoded_any = true;
+        const int32_t cp2 = (int32_t)(gb_tell(g.bz) >> 16);
+        if (cp2 != prev) { prev = cp2; ++b; }
+      }
+      if (rc < 0) {
+        if (rc == HBAM_EFORMAT || rc == HBAM_ETRUNC || rc == HBAM_ERUNTIMEIO || rc == HBAM_EREFID)
+          continue;
+        if (rc == HBAM_EEOF) {
+          if (!decoded_any && g.in.pos == g.in.len) continue;
+        } else {
+          *err = rc;
+          return end;
+        }
+      } else if (b < 3) {
+        if (!decoded_any) continue;
+      }
+      return (int64_t)((uint64_t)(beg + cp0) << 16 | (uint32_t)up0);
+    }
+  }
+}
+
+__device__ void crc_table_init(uint32_t* T) {
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1u) ? 0xedb88320u ^ (c >> 1) : c >> 1;
+    T[i] = c;
+  }
+  __syncthreads();
+}
+
+// One lane per guess.  bufs[i] = initial 8-byte ByteBuffer state; written back at exit.
+__global__ __launch_bounds__(GUESS_WG) void k_guess_bam(const uint8_t* __restrict__ file, int64_t flen,
+                                                        const int64_t* __restrict__ beg,
+                                                        const int64_t* __restrict__ end, uint32_t k,
+                                                        int32_t n_ref, uint8_t* __restrict__ scratch,
+                                                        uint8_t* __restrict__ lens_scratch,
+                                                        uint8_t* __restrict__ bufs,
+                                                        int64_t* __restrict__ out,
+                                                        int32_t* __restrict__ err) {
+  __shared__ uint16_t s_ll[GUESS_WG * 288];
+  __shared__ uint8_t s_d[GUESS_WG * 32];
+  __shared__ uint32_t T[256];
+  crc_table_init(T);
+  const uint32_t i = blockIdx.x * GUESS_WG + threadIdx.x;
+  if (i >= k) return;
+  Guesser g;
+  g.n_ref = n_ref;
+  for (int j = 0; j < 8; ++j) g.buf[j] = bufs[8 * (uint64_t)i + j];
+  g.bz.cur = scratch + (uint64_t)i * 65536;
+  g.bz.s_ll = s_ll + threadIdx.x * 288;
+  g.bz.s_d = s_d + threadIdx.x * 32;
+  g.bz.lens = lens_scratch + (uint64_t)i * LENS_SLOT;
+  g.bz.crc_tab = T;
+  g.bz.check_crc = 1;
+  int32_t e;
+  out[i] = g_guess(g, file, flen, beg[i], end[i], &e);
+  err[i] = e;
+  for (int j = 0; j < 8; ++j) bufs[8 * (uint64_t)i + j] = g.buf[j];
+}
+
+// BGZFSplitGuesser.guessNextBGZFBlockStart :51-92 (its own scan :95-148, IOExceptions escape)
+__global__ __launch_bounds__(GUESS_WG) void k_guess_bgzf(const uint8_t* __restrict__ file, int64_t flen,
+                                                         const int64_t* __restrict__ beg,
+                                                         const int64_t* __restrict__ end, uint32_t k,
+                                                         uint8_t* __restrict__ scratch,
+                                                         uint8_t* __restrict__ lens_scratch,
+                                                         int64_t* __restrict__ out,
+                                                         int32_t* __restrict__ err) {
+  __shared__ uint16_t s_ll[GUESS_WG * 288];
+  __shared__ uint8_t s_d[GUESS_WG * 32];
+  __shared__ uint32_t T[256];
+  crc_table_init(T);
+  const uint32_t i = blockIdx.x * GUESS_WG + threadIdx.x;
+  if (i >= k) return;
+  const int64_t b0 = beg[i], e0 = end[i];
+  int32_t want = (int32_t)(e0 - b0);
+  if (want > 2 * 0xffff - 1) want = 2 * 0xffff - 1;
+  int64_t total = 0;
+  if (want > 0 && b0 >= 0 && b0 <= flen) total = (flen - b0 < want) ? flen - b0 : want;
+  GStream in{file + ((b0 >= 0 && b0 <= flen) ? b0 : 0), total, 0};
+  GBcis bz;
+  bz.block_addr = 0;
+  bz.last_len = 0;
+  bz.cur_len = -1;
+  bz.cur_off = 0;
+  bz.cur = scratch + (uint64_t)i * 65536;
+  bz.s_ll = s_ll + threadIdx.x * 288;
+  bz.s_d = s_d + threadIdx.x * 32;
+  bz.lens = lens_scratch + (uint64_t)i * LENS_SLOT;
+  bz.crc_tab = T;
+  bz.check_crc = 1;
+  uint8_t buf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int32_t first_end = (int32_t)(e0 - b0);
+  if (first_end > 0xffff) first_end = 0xffff;
+  int64_t result = e0;
+  int32_t e = HBAM_OK;
+  auto i32 = [&](int o) {
+    return (int32_t)((uint32_t)buf[o] | (uint32_t)buf[o + 1] << 8 | (uint32_t)buf[o + 2] << 16 |
+                     (uint32_t)buf[o + 3] << 24);
+  };
+  for (int32_t pos = 0;;) {
+    int32_t p = pos;
+    bool found = false, notfound = false;
+    for (;;) {
+      for (;;) {
+        if (!gs_seek(in, p)) { e = HBAM_EIO; goto done; }
+        gs_read(in, buf, 4);
+        const int32_t n = i32(0);
+        if (n == G_MAGIC) break;
+        if ((int32_t)((uint32_t)n >> 8) == 0x00088b1f) ++p;
+        else if ((int32_t)((uint32_t)n >> 16) == 0x00008b1f) p += 2;
+        else p += 3;
+        if (p >= first_end) { notfound = true; break; }
+      }
+      if (notfound) break;
+      const int32_t p0 = p;
+      p += 10;
+      if (!gs_seek(in, p)) { e = HBAM_EIO; goto done; }
+      gs_read(in, buf, 2);
+      p += 2;
+      const int32_t xlen = (int32_t)(buf[0] | buf[1] << 8);
+      const int32_t sub_end = p + xlen;
+      while (p < sub_end) {
+        gs_read(in, buf, 4);
+        if (i32(0) != G_MAGIC_SUB) {
+          p += 4 + (int32_t)(buf[2] | buf[3] << 8);
+          if (!gs_seek(in, p)) { e = HBAM_EIO; goto done; }
+          continue;
+        }
+        pos = p0;
+        found = true;
+        break;
+      }
+      if (found) break;
+      p = p0 + 4;
+    }
+    if (notfound) { result = e0; break; }
+    if (gb_seek(bz, in, (uint64_t)(uint32_t)pos << 16)) { ++pos; continue; }
+    result = b0 + pos;
+    break;
+  }
+done:
+  out[i] = result;
+  err[i] = e;
+}
+
+}  // namespace hbam

@@ -1,0 +1,619 @@
+// hbam_kernels.hip — MI355X (gfx950) kernels of the BAM read path.
+//
+// Stage map (SURVEY.md §2.1 build units -> reference hot loops):
+//   K1 k_scan_chunks/k_gather_cands/k_verify_chain  BGZF framing   [htsjdk] BCIS.readBlock header
+//                                                    parse; BGZFBlockIndexer.skipBlock :130-181
+//   K2 k_inflate                                     [htsjdk] BlockGunzipper.unzipBlock (zlib)
+//      k_crc32                                       CRC32 check (BCIS.setCheckCrcs)
+//   K5 k_block_entry/k_block_walk/k_chain_fix/k_emit record boundaries: BAMRecordReader
+//                                                    .nextKeyValue loop :172-188 -> decode()
+//   K6/K7 k_decode_fixed / k_decode_pools            [htsjdk] BAMRecordCodec.decode + BAMRecord
+//                                                    lazy getters; BAMRecordReader.getKey :66-106
+//                                                    + MurmurHash3.murmurhash3 :32-102
+//   K8 (in k_decode_fixed)                           split bound, BAMRecordReader.java:173
+//
+// Memory layout in HBM: comp = compressed file bytes (+64 B pad); ubuf = concatenation of
+// the inflated blocks of the split (block b at uoff[b]); record starts rec_off (u64) into
+// ubuf; struct-of-arrays columns; variable-length pools addressed by exclusive scans.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "inflate_dev.h"
+#include "hbam_internal.h"
+
+namespace hbam {
+
+static __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) {
+  return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+static __device__ __forceinline__ uint16_t ld_u16_unaligned(const uint8_t* p) {
+  return (uint16_t)(p[0] | p[1] << 8);
+}
+
+// ------------------------------------------------------------------------------------
+// K1: candidate BGZF block starts.  htsjdk accepts a block when bytes 0..3 = 1f 8b 08 04
+// and XLEN (u16 @10) == 6 (BlockGunzipper; SI1/SI2/SLEN are skipped unchecked); the block
+// length is BSIZE (u16 @16) + 1.  One workgroup scans a SCAN_CHUNK-byte chunk; candidates
+// are collected in LDS, sorted, and written to a per-chunk slot (cap SCAN_CAP).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_scan_chunks(const uint8_t* __restrict__ comp,
+                                                     uint64_t begin, uint64_t end,
+                                                     uint32_t* __restrict__ chunk_cnt,
+                                                     uint64_t* __restrict__ chunk_pos,
+                                                     uint32_t* __restrict__ overflow) {
+  __shared__ uint32_t s_cnt;
+  __shared__ uint64_t s_pos[SCAN_CAP];
+  const uint64_t chunk = blockIdx.x;
+  const uint64_t c0 = begin + chunk * SCAN_CHUNK;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  // each thread tests 16 consecutive positions per step using a 32-byte window
+  for (uint32_t step = 0; step < SCAN_CHUNK / (256 * 16); ++step) {
+    const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * 16;
+    if (p0 >= end) break;
+    // 16-byte aligned relative to comp (begin is 16-aligned by construction of callers? no:
+    // use byte loads for the window to stay alignment-agnostic)
+    uint32_t w[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint64_t p = p0 + k;
+      if (p + 18 > end) break;
+      // bytes p..p+3 and p+10..p+11
+      const int q = k >> 2, r = k & 3;
+      const uint64_t lo = (uint64_t)w[q] | (uint64_t)w[q + 1] << 32;
+      const uint32_t m = (uint32_t)(lo >> (8 * r));
+      const uint64_t lo2 = (uint64_t)w[(k + 8) >> 2] | (uint64_t)w[((k + 8) >> 2) + 1] << 32;
+      const uint32_t x = (uint32_t)(lo2 >> (8 * ((k + 8) & 3)));  // bytes p+8..p+11
+      if (m == 0x04088b1fu && (x >> 16) == 6u) {
+        const uint32_t i = atomicAdd(&s_cnt, 1u);
+        if (i < SCAN_CAP) s_pos[i] = p;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t n = s_cnt;
+    if (n > SCAN_CAP) {
+      atomicOr(overflow, 1u);
+      n = SCAN_CAP;
+    }
+    // insertion sort (n is tiny: ~2-3 true blocks per 64 KiB)
+    for (uint32_t i = 1; i < n; ++i) {
+      const uint64_t v = s_pos[i];
+      uint32_t j = i;
+      while (j > 0 && s_pos[j - 1] > v) { s_pos[j] = s_pos[j - 1]; --j; }
+      s_pos[j] = v;
+    }
+    chunk_cnt[chunk] = n;
+    for (uint32_t i = 0; i < n; ++i) chunk_pos[chunk * SCAN_CAP + i] = s_pos[i];
+  }
+}
+
+__global__ void k_gather_cands(const uint32_t* __restrict__ chunk_cnt,
+                               const uint64_t* __restrict__ chunk_base,
+                               const uint64_t* __restrict__ chunk_pos, uint64_t nchunks,
+                               uint64_t* __restrict__ cand) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  const uint32_t n = chunk_cnt[c];
+  const uint64_t b = chunk_base[c];
+  for (uint32_t i = 0; i < n; ++i) cand[b + i] = chunk_pos[c * SCAN_CAP + i];
+}
+
+// Chain check: cand[0] must be the chain start; every candidate's successor
+// (pos + BSIZE + 1) must be the next candidate (or the data end for the last).  Fills the
+// block table on the way.
+__global__ void k_verify_chain(const uint8_t* __restrict__ comp, const uint64_t* __restrict__ cand,
+                               uint64_t n, uint64_t data_end, BlockRec* __restrict__ blk,
+                               uint32_t* __restrict__ bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t p = cand[i];
+  const uint32_t bl = (uint32_t)ld_u16_unaligned(comp + p + 16) + 1u;
+  const uint64_t nx = p + bl;
+  bool ok = (i + 1 < n) ? (nx == cand[i + 1]) : (nx <= data_end);
+  BlockRec r;
+  r.coff = p;
+  r.clen = bl;
+  if (nx <= data_end && bl >= 18) {
+    r.crc = ld_u32_unaligned(comp + p + bl - 8);
+    r.isize = ld_u32_unaligned(comp + p + bl - 4);
+  } else {
+    r.crc = 0;
+    r.isize = 0;
+    ok = false;
+  }
+  blk[i] = r;
+  if (!ok) atomicAdd(bad, 1u);
+}
+
+// ------------------------------------------------------------------------------------
+// K2: inflate, one lane per BGZF block (SIMT across blocks).  LDS: per lane 288 u16 +
+// 32 u8 symbol slots.  Block status: INF_* codes (header checks are done at scan time).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(INFLATE_WG) void k_inflate(const uint8_t* __restrict__ comp,
+                                                        const BlockRec* __restrict__ blk,
+                                                        const uint64_t* __restrict__ uoff,
+                                                        uint32_t nblk, uint8_t* __restrict__ ubuf,
+                                                        uint8_t* __restrict__ lens_scratch,
+                                                        int32_t* __restrict__ status) {
+  __shared__ uint16_t s_ll[INFLATE_WG * 288];
+  __shared__ uint8_t s_d[INFLATE_WG * 32];
+  const uint32_t b = blockIdx.x * INFLATE_WG + threadIdx.x;
+  if (b >= nblk) return;
+  const BlockRec r = blk[b];
+  uint32_t produced = 0;
+  int32_t st;
+  if (r.isize > 65536u) {
+    st = INF_OK;  // unsupported here; the runtime reports HBAM_EUNSUPPORTED for it
+  } else if (r.clen < 26u) {
+    st = INF_DATA;  // Inflater.setInput with a negative length
+  } else {
+    st = inflate_raw(comp + r.coff + 18, r.clen - 26u, ubuf + uoff[b], r.isize,
+                     s_ll + threadIdx.x * 288, s_d + threadIdx.x * 32,
+                     lens_scratch + (uint64_t)b * LENS_SLOT, &produced);
+  }
+  status[b] = st;
+}
+
+// CRC-32 (IEEE, reflected 0xEDB88320) of each inflated block, slice-by-4 tables in LDS.
+__global__ __launch_bounds__(256) void k_crc32(const BlockRec* __restrict__ blk,
+                                               const uint64_t* __restrict__ uoff, uint32_t nblk,
+                                               const uint8_t* __restrict__ ubuf,
+                                               uint32_t* __restrict__ crc_out) {
+  __shared__ uint32_t T[4][256];
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1u) ? 0xedb88320u ^ (c >> 1) : c >> 1;
+    T[0][i] = c;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = T[0][i];
+    c = T[0][c & 0xff] ^ (c >> 8); T[1][i] = c;
+    c = T[0][c & 0xff] ^ (c >> 8); T[2][i] = c;
+    c = T[0][c & 0xff] ^ (c >> 8); T[3][i] = c;
+  }
+  __syncthreads();
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  const uint8_t* p = ubuf + uoff[b];
+  uint32_t n = blk[b].isize;
+  uint32_t c = 0xffffffffu;
+  while (n && ((uintptr_t)p & 3u)) { c = T[0][(c ^ *p++) & 0xff] ^ (c >> 8); --n; }
+  const uint32_t* w = (const uint32_t*)p;
+  for (; n >= 4; n -= 4) {
+    c ^= *w++;
+    c = T[3][c & 0xff] ^ T[2][(c >> 8) & 0xff] ^ T[1][(c >> 16) & 0xff] ^ T[0][c >> 24];
+  }
+  p = (const uint8_t*)w;
+  while (n--) c = T[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+  crc_out[b] = ~c;
+}
+
+// ------------------------------------------------------------------------------------
+// K5: record boundaries over the inflated stream.  Chain: r_{k+1} = r_k + 4 + block_size_k.
+// Per block: find an entry candidate (first offset passing a strict record predicate
+// plus a short chain check), walk to the block end, then stitch: entry[b] must equal
+// exit[b-1]; mismatches are re-walked in order by k_chain_fix.
+// ------------------------------------------------------------------------------------
+static __device__ __forceinline__ bool rec_plausible(const uint8_t* __restrict__ u, uint64_t x,
+                                                     uint64_t hard_end, int32_t n_ref) {
+  if (x + 36 > hard_end) return false;
+  const uint8_t* p = u + x;
+  const int32_t bs = (int32_t)ld_u32_unaligned(p);
+  const int32_t id = (int32_t)ld_u32_unaligned(p + 4);
+  const int32_t pos = (int32_t)ld_u32_unaligned(p + 8);
+  const uint32_t L = p[12];
+  const uint32_t ncig = ld_u16_unaligned(p + 16);
+  const int32_t lseq = (int32_t)ld_u32_unaligned(p + 20);
+  const int32_t nid = (int32_t)ld_u32_unaligned(p + 24);
+  const int32_t npos = (int32_t)ld_u32_unaligned(p + 28);
+  if (bs < 32 || id < -1 || id >= n_ref || nid < -1 || nid >= n_ref || pos < -1 || npos < -1)
+    return false;
+  if (L == 0 || lseq < 0) return false;
+  const int64_t need = 32 + (int64_t)L + 4 * (int64_t)ncig + (int64_t)lseq + ((int64_t)lseq + 1) / 2;
+  if ((int64_t)bs < need) return false;
+  if (x + 36 + L > hard_end) return false;
+  return p[36 + L - 1] == 0;
+}
+
+__global__ __launch_bounds__(64) void k_block_entry(const uint8_t* __restrict__ u,
+                                                    const uint64_t* __restrict__ uoff, uint32_t nblk,
+                                                    uint64_t hard_end, int32_t n_ref,
+                                                    uint64_t* __restrict__ entry) {
+  const uint32_t b = blockIdx.x + 1;  // block 0's entry is the split start
+  if (b >= nblk) return;
+  const uint64_t b0 = uoff[b], b1 = uoff[b + 1];
+  const uint32_t lane = threadIdx.x;
+  uint64_t found = NO_ENTRY;
+  for (uint64_t x0 = b0; x0 < b1 && found == NO_ENTRY; x0 += 64) {
+    const uint64_t x = x0 + lane;
+    const bool c = (x < b1) && rec_plausible(u, x, hard_end, n_ref);
+    uint64_t mask = __ballot(c);
+    while (mask) {
+      const int l = __ffsll((unsigned long long)mask) - 1;
+      mask &= mask - 1;
+      const uint64_t xc = x0 + (uint64_t)l;
+      // chain check: up to 3 further hops must be plausible or end exactly at hard_end
+      bool ok = true;
+      if (lane == 0) {
+        uint64_t r = xc;
+        for (int h = 0; h < 3 && ok; ++h) {
+          const int32_t bs = (int32_t)ld_u32_unaligned(u + r);
+          r += 4 + (uint64_t)(uint32_t)bs;
+          if (r == hard_end) break;
+          ok = rec_plausible(u, r, hard_end, n_ref);
+        }
+      }
+      ok = __shfl(ok, 0);
+      if (ok) { found = xc; break; }
+    }
+  }
+  if (lane == 0) entry[b] = found;
+}
+
+// Walk block b from entry[b]: record starts in [uoff[b], uoff[b+1]) are stored as u16
+// offsets (cap WALK_CAP per block); exit[b] = first chain position >= uoff[b+1], or
+// CHAIN_STOP when a record's block_size cannot be read / is < 32 (chain ends there).
+static __device__ void walk_one(const uint8_t* __restrict__ u, const uint64_t* __restrict__ uoff,
+                                uint32_t b, uint64_t r, uint64_t hard_end,
+                                uint16_t* __restrict__ rel, uint32_t* __restrict__ count,
+                                uint64_t* __restrict__ exitp) {
+  const uint64_t b0 = uoff[b], b1 = uoff[b + 1];
+  uint32_t n = 0;
+  if (r == NO_ENTRY) {
+    count[b] = 0;
+    exitp[b] = NO_ENTRY;
+    return;
+  }
+  if (r == CHAIN_STOP) {
+    count[b] = 0;
+    exitp[b] = CHAIN_STOP;
+    return;
+  }
+  while (r < b1) {
+    if (n < WALK_CAP) rel[(uint64_t)b * WALK_CAP + n] = (uint16_t)(r - b0);
+    ++n;
+    if (r + 4 > hard_end) { r = CHAIN_STOP; break; }
+    const int32_t bs = (int32_t)ld_u32_unaligned(u + r);
+    if (bs < 32) { r = CHAIN_STOP; break; }
+    r += 4 + (uint64_t)(uint32_t)bs;
+  }
+  count[b] = n;
+  exitp[b] = r;
+}
+
+__global__ void k_block_walk(const uint8_t* __restrict__ u, const uint64_t* __restrict__ uoff,
+                             uint32_t nblk, uint64_t r0, uint64_t hard_end,
+                             const uint64_t* __restrict__ entry, uint16_t* __restrict__ rel,
+                             uint32_t* __restrict__ count, uint64_t* __restrict__ exitp) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  const uint64_t r = (b == 0) ? r0 : entry[b];
+  walk_one(u, uoff, b, r, hard_end, rel, count, exitp);
+}
+
+// mismatch list: blocks whose entry != predecessor's exit
+__global__ void k_stitch_check(const uint64_t* __restrict__ entry, const uint64_t* __restrict__ exitp,
+                               uint32_t nblk, uint32_t* __restrict__ nbad,
+                               uint32_t* __restrict__ bad_list, uint32_t cap) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (b >= nblk) return;
+  if (entry[b] != exitp[b - 1]) {
+    const uint32_t i = atomicAdd(nbad, 1u);
+    if (i < cap) bad_list[i] = b;
+  }
+}
+
+// Sequential repair (one lane): process mismatched blocks in order, re-walking from the
+// predecessor's exit and propagating until consistent again.
+__global__ void k_chain_fix(const uint8_t* __restrict__ u, const uint64_t* __restrict__ uoff,
+                            uint32_t nblk, uint64_t hard_end, uint64_t* __restrict__ entry,
+                            uint16_t* __restrict__ rel, uint32_t* __restrict__ count,
+                            uint64_t* __restrict__ exitp, const uint32_t* __restrict__ bad_list,
+                            uint32_t nbad) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t done_upto = 0;  // blocks < done_upto are consistent
+  for (uint32_t i = 0; i < nbad; ++i) {
+    uint32_t b = bad_list[i];
+    if (b < done_upto) continue;
+    while (b < nblk && entry[b] != exitp[b - 1]) {
+      const uint64_t e = exitp[b - 1];
+      entry[b] = e;
+      walk_one(u, uoff, b, e, hard_end, rel, count, exitp);
+      ++b;
+    }
+    done_upto = b;
+  }
+}
+
+__global__ void k_emit_offsets(const uint64_t* __restrict__ uoff, const BlockRec* __restrict__ blk,
+                               uint32_t nblk, const uint16_t* __restrict__ rel,
+                               const uint32_t* __restrict__ count, const uint64_t* __restrict__ base,
+                               uint64_t* __restrict__ rec_off, uint64_t* __restrict__ voffset) {
+  const uint32_t b = blockIdx.x;
+  if (b >= nblk) return;
+  const uint32_t n = count[b] < WALK_CAP ? count[b] : WALK_CAP;
+  const uint64_t o = base[b];
+  const uint64_t u0 = uoff[b];
+  const uint64_t cv = blk[b].coff << 16;
+  for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+    const uint32_t r = rel[(uint64_t)b * WALK_CAP + k];
+    rec_off[o + k] = u0 + r;
+    voffset[o + k] = cv | r;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// K6/K7/K8: fixed-field decode, per-record status, coordinate key, pool lengths.
+// ------------------------------------------------------------------------------------
+static __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return x << r | x >> (64 - r); }
+static __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+static __device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t* p) {
+  return (uint64_t)ld_u32_unaligned(p) | (uint64_t)ld_u32_unaligned(p + 4) << 32;
+}
+// MurmurHash3.murmurhash3(byte[], seed=0) incl. the h2 quirk of MurmurHash3.java:59
+static __device__ uint64_t murmur3_java(const uint8_t* __restrict__ key, int32_t len) {
+  const int32_t nblocks = len / 16;
+  uint64_t h1 = 0, h2 = 0;
+  const uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+  for (int32_t i = 0; i < nblocks; ++i) {
+    uint64_t k1 = ld_u64_unaligned(key + 16 * i), k2 = ld_u64_unaligned(key + 16 * i + 8);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = h2 << 31 | h1 >> 33;
+    h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+  }
+  const uint8_t* tail = key + 16 * nblocks;
+  const int32_t t = len & 15;
+  uint64_t k1 = 0, k2 = 0;
+  for (int32_t i = t - 1; i >= 8; --i) k2 ^= (uint64_t)tail[i] << (8 * (i - 8));
+  if (t > 8) { k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2; }
+  for (int32_t i = (t < 8 ? t : 8) - 1; i >= 0; --i) k1 ^= (uint64_t)tail[i] << (8 * i);
+  if (t > 0) { k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1; }
+  h1 ^= (uint64_t)(int64_t)len;
+  h2 ^= (uint64_t)(int64_t)len;
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  h1 += h2;
+  return h1;
+}
+
+// Event model of BlockCompressedInputStream (SURVEY.md A.2, 1.131 semantics): a read()
+// call that starts exactly where an empty BGZF block follows returns -1; empty blocks
+// strictly inside a read are transparent; the hard end H (end of data, or the first block
+// that fails to read) ends every read.  decode() issues one read per field.
+static __device__ __forceinline__ bool empty_at(const uint64_t* __restrict__ ev, uint32_t nev,
+                                                uint64_t p) {
+  for (uint32_t i = 0; i < nev; ++i)
+    if (ev[i] == p) return true;
+  return false;
+}
+
+__global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,
+                               const uint64_t* __restrict__ rec_off,
+                               const uint64_t* __restrict__ voffset, uint64_t v_end,
+                               uint64_t hard_end, int32_t hard_code,
+                               const uint64_t* __restrict__ ev, uint32_t nev, int32_t n_ref,
+                               int32_t validate_refs, DevColumns c,
+                               unsigned long long* __restrict__ first_stop) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrec) return;
+  const uint64_t r = rec_off[i];
+  int32_t st = ST_OK;
+  // split bound (nextKeyValue :173): checked before decode()
+  if ((int64_t)voffset[i] >= (int64_t)v_end) {
+    st = ST_VEND;
+  } else if (empty_at(ev, nev, r)) {
+    st = ST_NULL;
+  } else if (hard_end < r + 4) {
+    st = (hard_code == HBAM_EEOF) ? ST_NULL : hard_code;
+  }
+  int32_t bs = 0;
+  if (st == ST_OK) {
+    bs = (int32_t)ld_u32_unaligned(u + r);
+    if (bs < 32) st = HBAM_EFORMAT;
+  }
+  if (st == ST_OK && nev) {
+    // read() calls of decode(): block_size | refID | pos | l_read_name | MAPQ | bin |
+    // n_cigar | flag | l_seq | next_refID | next_pos | tlen | rest (only if bs > 32)
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      const uint32_t o = k == 0 ? 4 : k == 1 ? 8 : k == 2 ? 12 : k == 3 ? 13 : k == 4 ? 14
+                       : k == 5 ? 16 : k == 6 ? 18 : k == 7 ? 20 : k == 8 ? 24 : k == 9 ? 28
+                       : k == 10 ? 32 : 36;
+      if (k == 11 && bs <= 32) break;
+      if (st == ST_OK && r + o <= hard_end && empty_at(ev, nev, r + o)) st = HBAM_EEOF;
+    }
+  }
+  if (st == ST_OK && hard_end < r + 4 + (uint64_t)(uint32_t)bs) st = hard_code;
+  int32_t ref = 0, pos = 0, lseq = 0, nref = 0, npos = 0, tlen = 0;
+  uint8_t lrn = 0, mapq = 0;
+  uint16_t bin = 0, ncig = 0, flag = 0;
+  if (st == ST_OK) {
+    const uint8_t* p = u + r;
+    ref = (int32_t)ld_u32_unaligned(p + 4);
+    pos = (int32_t)ld_u32_unaligned(p + 8);
+    lrn = p[12];
+    mapq = p[13];
+    bin = ld_u16_unaligned(p + 14);
+    ncig = ld_u16_unaligned(p + 16);
+    flag = ld_u16_unaligned(p + 18);
+    lseq = (int32_t)ld_u32_unaligned(p + 20);
+    nref = (int32_t)ld_u32_unaligned(p + 24);
+    npos = (int32_t)ld_u32_unaligned(p + 28);
+    tlen = (int32_t)ld_u32_unaligned(p + 32);
+    if (validate_refs && ((ref != -1 && (ref < 0 || ref >= n_ref)) ||
+                          (nref != -1 && (nref < 0 || nref >= n_ref))))
+      st = HBAM_EREFID;
+  }
+  if (st != ST_OK) {
+    atomicMin(first_stop, (unsigned long long)i);
+    c.status[i] = st;
+    c.name_len[i] = 0;
+    c.cigar_n[i] = 0;
+    c.seq_len[i] = 0;
+    c.aux_len[i] = 0;
+    return;
+  }
+  c.status[i] = ST_OK;
+  c.block_size[i] = bs;
+  c.ref_id[i] = ref;
+  c.pos[i] = pos;
+  c.l_read_name[i] = lrn;
+  c.mapq[i] = mapq;
+  c.bin[i] = bin;
+  c.n_cigar[i] = ncig;
+  c.flag[i] = flag;
+  c.l_seq[i] = lseq;
+  c.next_ref_id[i] = nref;
+  c.next_pos[i] = npos;
+  c.tlen[i] = tlen;
+  // key: BAMRecordReader.getKey(SAMRecord) :66-96
+  const int32_t start = (int32_t)((uint32_t)pos + 1u);
+  int64_t key;
+  if (!((flag & 4) || ref < 0 || start < 0)) {
+    key = (int64_t)((uint64_t)(int64_t)ref << 32 | (uint64_t)(int64_t)pos);
+  } else {
+    const int32_t h = (int32_t)murmur3_java(u + r + 36, bs - 32);
+    key = (int64_t)((uint64_t)0x7fffffffULL << 32 | (uint64_t)(int64_t)h);
+  }
+  c.key[i] = key;
+  // variable-block layout: name | cigar | seq (packed) | qual | aux
+  const int64_t var = (int64_t)bs - 32;
+  const int64_t fixed_var = (int64_t)lrn + 4 * (int64_t)ncig + ((int64_t)lseq + 1) / 2 + (int64_t)lseq;
+  if (lseq < 0 || fixed_var > var) {
+    c.layout_ok[i] = 0;
+    c.name_len[i] = 0;
+    c.cigar_n[i] = 0;
+    c.seq_len[i] = 0;
+    c.aux_len[i] = 0;
+  } else {
+    c.layout_ok[i] = 1;
+    c.name_len[i] = lrn;
+    c.cigar_n[i] = ncig;
+    c.seq_len[i] = (uint32_t)lseq;
+    c.aux_len[i] = (uint32_t)(var - fixed_var);
+  }
+}
+
+// Pools: names (l_read_name bytes incl. NUL), CIGAR u32s, SEQ unpacked to
+// "=ACMGRSVTWYHKDBN", QUAL raw, AUX raw.  One wave per record, lanes copy bytes.
+__global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict__ u, uint64_t nrec,
+                                                      const uint64_t* __restrict__ rec_off,
+                                                      DevColumns c) {
+  const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (i >= nrec) return;
+  if (!c.layout_ok[i]) return;
+  const uint8_t* p = u + rec_off[i] + 36;
+  const uint32_t nl = c.name_len[i], nc = c.cigar_n[i], ls = c.seq_len[i], na = c.aux_len[i];
+  uint8_t* dn = c.names + c.name_off[i];
+  for (uint32_t k = lane; k < nl; k += 64) dn[k] = p[k];
+  p += nl;
+  uint32_t* dc = c.cigars + c.cigar_off[i];
+  for (uint32_t k = lane; k < nc; k += 64) dc[k] = ld_u32_unaligned(p + 4 * k);
+  p += 4 * nc;
+  uint8_t* ds = c.seq + c.seq_off[i];
+  const char* alpha = "=ACMGRSVTWYHKDBN";
+  for (uint32_t k = lane; k < ls; k += 64) {
+    const uint8_t b = p[k >> 1];
+    ds[k] = (uint8_t)alpha[(k & 1) ? (b & 15) : (b >> 4)];
+  }
+  p += (ls + 1) / 2;
+  uint8_t* dq = c.qual + c.seq_off[i];
+  for (uint32_t k = lane; k < ls; k += 64) dq[k] = p[k];
+  p += ls;
+  uint8_t* da = c.aux + c.aux_off[i];
+  for (uint32_t k = lane; k < na; k += 64) da[k] = p[k];
+}
+
+// ------------------------------------------------------------------------------------
+// scans (u32 -> u64 exclusive), 3-phase reduce-then-scan
+// ------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(SCAN_WG) void k_scan_reduce(const T* __restrict__ in, uint64_t n,
+                                                         uint64_t* __restrict__ partial) {
+  __shared__ uint64_t s[SCAN_WG];
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+  uint64_t acc = 0;
+  for (uint32_t k = threadIdx.x; k < SCAN_TILE; k += SCAN_WG) {
+    const uint64_t j = base + k;
+    if (j < n) acc += (uint64_t)in[j];
+  }
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t o = SCAN_WG / 2; o; o >>= 1) {
+    if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = s[0];
+}
+
+__global__ __launch_bounds__(SCAN_WG) void k_scan_partials(uint64_t* __restrict__ partial,
+                                                           uint64_t n, uint64_t* __restrict__ total) {
+  __shared__ uint64_t s[SCAN_WG];
+  uint64_t carry = 0;
+  for (uint64_t base = 0; base < n; base += SCAN_WG) {
+    const uint64_t j = base + threadIdx.x;
+    const uint64_t v = j < n ? partial[j] : 0;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < SCAN_WG; o <<= 1) {
+      const uint64_t t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+      __syncthreads();
+      s[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (j < n) partial[j] = carry + s[threadIdx.x] - v;
+    const uint64_t tot = s[SCAN_WG - 1];
+    __syncthreads();
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+template <typename T>
+__global__ __launch_bounds__(SCAN_WG) void k_scan_apply(const T* __restrict__ in, uint64_t n,
+                                                        const uint64_t* __restrict__ partial,
+                                                        uint64_t* __restrict__ out) {
+  __shared__ uint64_t s[SCAN_WG];
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+  uint64_t carry = partial[blockIdx.x];
+  for (uint32_t t0 = 0; t0 < SCAN_TILE; t0 += SCAN_WG) {
+    const uint64_t j = base + t0 + threadIdx.x;
+    const uint64_t v = j < n ? (uint64_t)in[j] : 0;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < SCAN_WG; o <<= 1) {
+      const uint64_t t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+      __syncthreads();
+      s[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (j < n) out[j] = carry + s[threadIdx.x] - v;
+    const uint64_t tot = s[SCAN_WG - 1];
+    __syncthreads();
+    carry += tot;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = carry;
+}
+
+// explicit instantiations used by the runtime
+template __global__ void k_scan_reduce<uint32_t>(const uint32_t*, uint64_t, uint64_t*);
+template __global__ void k_scan_apply<uint32_t>(const uint32_t*, uint64_t, const uint64_t*, uint64_t*);
+
+}  // namespace hbam

@@ -1,0 +1,314 @@
+"""ctypes binding of libhbam.so (include/hbam.h).
+
+The product path is the HIP library only: if libhbam.so is missing or cannot create a
+device context, calls raise HbamUnavailable — there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # hadoop-bam_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "libhbam.so")
+
+HBAM_OK = 0
+HBAM_EIO = -1
+HBAM_ETRUNC = -2
+HBAM_EFORMAT = -3
+HBAM_ERUNTIMEIO = -4
+HBAM_EEOF = -5
+HBAM_EREFID = -6
+HBAM_EDATA = -7
+HBAM_ENOMEM = -8
+HBAM_EUNSUPPORTED = -9
+HBAM_EDEVICE = -10
+HBAM_EINVAL = -11
+HBAM_EMORE = -12
+
+CODE_NAMES = {
+    HBAM_OK: "OK", HBAM_EIO: "IOException", HBAM_ETRUNC: "FileTruncatedException",
+    HBAM_EFORMAT: "SAMFormatException", HBAM_ERUNTIMEIO: "RuntimeIOException",
+    HBAM_EEOF: "RuntimeEOFException", HBAM_EREFID: "IllegalArgumentException",
+    HBAM_EDATA: "RuntimeException(DataFormatException)", HBAM_ENOMEM: "OutOfMemory",
+    HBAM_EUNSUPPORTED: "Unsupported", HBAM_EDEVICE: "DeviceError", HBAM_EINVAL: "InvalidArgument",
+    HBAM_EMORE: "NeedMoreData",
+}
+
+# every entry point include/hbam.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "hbam_create", "hbam_destroy", "hbam_last_error", "hbam_stream", "hbam_get_timing",
+    "hbam_upload", "hbam_device_free", "hbam_parse_header", "hbam_scan_blocks", "hbam_inflate",
+    "hbam_decode_split", "hbam_columns_to_host", "hbam_free_host_columns",
+    "hbam_release_columns", "hbam_guess_bam_record_start", "hbam_guess_batch",
+    "hbam_guess_bgzf_block_start", "hbam_probabilistic_splits",
+]
+
+
+class HbamUnavailable(RuntimeError):
+    pass
+
+
+class Opts(C.Structure):
+    _fields_ = [("check_crc", C.c_int32), ("validate_refs", C.c_int32),
+                ("reserved", C.c_int32 * 14)]
+
+
+class Header(C.Structure):
+    _fields_ = [("l_text", C.c_int32), ("n_ref", C.c_int32), ("header_ulen", C.c_uint64),
+                ("first_voffset", C.c_uint64)]
+
+
+class Block(C.Structure):
+    _fields_ = [("coff", C.c_uint64), ("clen", C.c_uint32), ("isize", C.c_uint32),
+                ("crc", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class Timing(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("scan_ms", "inflate_ms", "crc_ms", "walk_ms",
+                                          "decode_ms", "pools_ms", "total_ms")] + \
+               [(n, C.c_uint64) for n in ("n_blocks", "comp_bytes", "ubuf_bytes", "n_records",
+                                          "pool_bytes")]
+
+
+_u8p = C.POINTER(C.c_uint8)
+_u16p = C.POINTER(C.c_uint16)
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+
+
+class Columns(C.Structure):
+    _fields_ = [
+        ("n_records", C.c_uint64), ("status", C.c_int32), ("pad0", C.c_int32),
+        ("err_record", C.c_uint64), ("voffset", _u64p), ("key", _i64p), ("rec_off", _u64p),
+        ("ubuf", _u8p), ("ubuf_len", C.c_uint64), ("block_size", _i32p), ("ref_id", _i32p),
+        ("pos", _i32p), ("l_read_name", _u8p), ("mapq", _u8p), ("bin", _u16p),
+        ("n_cigar", _u16p), ("flag", _u16p), ("l_seq", _i32p), ("next_ref_id", _i32p),
+        ("next_pos", _i32p), ("tlen", _i32p), ("layout_ok", _u8p), ("name_off", _u64p),
+        ("names", _u8p), ("cigar_off", _u64p), ("cigars", _u32p), ("seq_off", _u64p),
+        ("seq", _u8p), ("qual", _u8p), ("aux_off", _u64p), ("aux", _u8p),
+    ]
+
+
+FIXED = [("voffset", np.uint64), ("key", np.int64), ("rec_off", np.uint64),
+         ("block_size", np.int32), ("ref_id", np.int32), ("pos", np.int32),
+         ("l_read_name", np.uint8), ("mapq", np.uint8), ("bin", np.uint16),
+         ("n_cigar", np.uint16), ("flag", np.uint16), ("l_seq", np.int32),
+         ("next_ref_id", np.int32), ("next_pos", np.int32), ("tlen", np.int32),
+         ("layout_ok", np.uint8)]
+
+_LIB = None
+
+
+def load(path=None):
+    """Load libhbam.so (raises HbamUnavailable if it is not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise HbamUnavailable("libhbam.so not built (run __graft_entry__.build())")
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    sig = {
+        "hbam_create": (vp, [C.c_int, C.POINTER(Opts)]),
+        "hbam_destroy": (None, [vp]),
+        "hbam_last_error": (C.c_char_p, [vp]),
+        "hbam_stream": (vp, [vp]),
+        "hbam_get_timing": (C.c_int, [vp, C.POINTER(Timing)]),
+        "hbam_upload": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(vp)]),
+        "hbam_device_free": (C.c_int, [vp, vp]),
+        "hbam_parse_header": (C.c_int, [vp, vp, C.c_int, C.c_uint64, C.POINTER(Header)]),
+        "hbam_scan_blocks": (C.c_int, [vp, vp, C.c_int, C.c_uint64, C.c_uint64,
+                                       C.POINTER(Block), C.c_uint64, C.POINTER(C.c_uint64)]),
+        "hbam_inflate": (C.c_int, [vp, vp, C.c_int, C.c_uint64, C.POINTER(Block), C.c_uint64,
+                                   C.c_int, vp, C.c_uint64, vp, vp]),
+        "hbam_decode_split": (C.c_int, [vp, vp, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
+                                        C.c_uint64, C.c_uint64, C.c_int32, C.POINTER(Columns)]),
+        "hbam_columns_to_host": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(Columns)]),
+        "hbam_free_host_columns": (None, [C.POINTER(Columns)]),
+        "hbam_release_columns": (None, [vp, C.POINTER(Columns)]),
+        "hbam_guess_bam_record_start": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_int64,
+                                                    C.c_int64, C.c_int32, _i32p]),
+        "hbam_guess_batch": (C.c_int, [vp, vp, C.c_int, C.c_uint64, vp, vp, C.c_uint64,
+                                       C.c_int32, vp, vp]),
+        "hbam_guess_bgzf_block_start": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_int64,
+                                                    C.c_int64, _i32p]),
+        "hbam_probabilistic_splits": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, vp, vp,
+                                                  C.c_uint64, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def host_columns_to_numpy(h):
+    """Copy a host hbam_columns into a dict of numpy arrays."""
+    n = int(h.n_records)
+    out = {"n": n, "status": int(h.status), "err_record": int(h.err_record)}
+    for name, dt in FIXED:
+        p = getattr(h, name)
+        out[name] = np.ctypeslib.as_array(p, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
+    for name in ("name_off", "cigar_off", "seq_off", "aux_off"):
+        p = getattr(h, name)
+        out[name] = np.ctypeslib.as_array(p, shape=(n + 1,)).copy() if p else np.zeros(1, np.uint64)
+    pools = [("names", np.uint8, "name_off"), ("cigars", np.uint32, "cigar_off"),
+             ("seq", np.uint8, "seq_off"), ("qual", np.uint8, "seq_off"),
+             ("aux", np.uint8, "aux_off")]
+    for name, dt, off in pools:
+        m = int(out[off][-1]) if n else 0
+        p = getattr(h, name)
+        out[name] = np.ctypeslib.as_array(p, shape=(m,)).astype(dt).copy() if m else np.zeros(0, dt)
+    return out
+
+
+class Context:
+    """One device context (hbam_ctx): a HIP stream plus device work buffers."""
+
+    def __init__(self, device=0, check_crc=False, validate_refs=True):
+        self.L = load()
+        o = Opts()
+        o.check_crc = int(check_crc)
+        o.validate_refs = int(validate_refs)
+        self.h = self.L.hbam_create(device, C.byref(o))
+        if not self.h:
+            raise HbamUnavailable("hbam_create failed: no HIP device %d" % device)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.hbam_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_error(self):
+        return self.L.hbam_last_error(self.h).decode(errors="replace")
+
+    def timing(self):
+        t = Timing()
+        self.L.hbam_get_timing(self.h, C.byref(t))
+        return {n: getattr(t, n) for n, _ in Timing._fields_}
+
+    @staticmethod
+    def _ptr(data):
+        """(pointer, length, on_device, keepalive) for bytes / numpy / torch cuda tensor."""
+        if hasattr(data, "data_ptr") and hasattr(data, "is_cuda"):
+            if data.is_cuda:
+                return C.c_void_p(data.data_ptr()), data.numel() * data.element_size(), 1, data
+            a = data.numpy()
+        elif isinstance(data, np.ndarray):
+            a = np.ascontiguousarray(data, dtype=np.uint8)
+        else:
+            a = np.frombuffer(bytes(data), dtype=np.uint8)
+        if a.size == 0:
+            a = np.zeros(1, np.uint8)
+            return C.c_void_p(a.ctypes.data), 0, 0, a
+        return C.c_void_p(a.ctypes.data), a.size, 0, a
+
+    def parse_header(self, data):
+        p, n, dev, keep = self._ptr(data)
+        h = Header()
+        rc = self.L.hbam_parse_header(self.h, p, dev, n, C.byref(h))
+        if rc:
+            return rc
+        return dict(l_text=h.l_text, n_ref=h.n_ref, header_ulen=h.header_ulen,
+                    first_voffset=h.first_voffset)
+
+    def scan_blocks(self, data, base_off=0):
+        p, n, dev, keep = self._ptr(data)
+        cap = n // 18 + 2
+        arr = (Block * cap)()
+        nb = C.c_uint64(0)
+        rc = self.L.hbam_scan_blocks(self.h, p, dev, n, base_off, arr, cap, C.byref(nb))
+        k = int(nb.value)
+        out = dict(coff=np.array([arr[i].coff for i in range(k)], np.uint64),
+                   clen=np.array([arr[i].clen for i in range(k)], np.uint32),
+                   isize=np.array([arr[i].isize for i in range(k)], np.uint32),
+                   crc=np.array([arr[i].crc for i in range(k)], np.uint32))
+        return rc, out
+
+    def inflate(self, data, blocks, check_crc=True):
+        p, n, dev, keep = self._ptr(data)
+        k = len(blocks["coff"])
+        arr = (Block * max(k, 1))()
+        for i in range(k):
+            arr[i].coff = int(blocks["coff"][i])
+            arr[i].clen = int(blocks["clen"][i])
+            arr[i].isize = int(blocks["isize"][i])
+            arr[i].crc = int(blocks["crc"][i])
+        total = int(np.sum(blocks["isize"], dtype=np.uint64)) if k else 0
+        out = np.zeros(max(total, 1), np.uint8)
+        off = np.zeros(k + 1, np.uint64)
+        st = np.zeros(max(k, 1), np.int32)
+        rc = self.L.hbam_inflate(self.h, p, dev, n, arr, k, int(check_crc),
+                                 out.ctypes.data, out.size, off.ctypes.data, st.ctypes.data)
+        return rc, out[:total], off, st[:k]
+
+    def decode_split(self, data, v_start, v_end, n_ref=-1, comp_base=0, file_len=None):
+        """BAMRecordReader over one FileVirtualSplit; returns host numpy columns."""
+        p, n, dev, keep = self._ptr(data)
+        if file_len is None:
+            file_len = comp_base + n
+        d = Columns()
+        rc = self.L.hbam_decode_split(self.h, p, dev, comp_base, n, file_len, v_start, v_end,
+                                      n_ref, C.byref(d))
+        if rc:
+            return {"rc": rc, "error": self.last_error()}
+        h = Columns()
+        rc = self.L.hbam_columns_to_host(self.h, C.byref(d), C.byref(h))
+        if rc:
+            return {"rc": rc, "error": self.last_error()}
+        out = host_columns_to_numpy(h)
+        self.L.hbam_free_host_columns(C.byref(h))
+        out["rc"] = 0
+        out["timing"] = self.timing()
+        return out
+
+    def decode_split_device(self, data, v_start, v_end, n_ref, comp_base=0, file_len=None):
+        """Device-resident decode (bench path): returns the hbam_columns struct."""
+        p, n, dev, keep = self._ptr(data)
+        if file_len is None:
+            file_len = comp_base + n
+        d = Columns()
+        rc = self.L.hbam_decode_split(self.h, p, dev, comp_base, n, file_len, v_start, v_end,
+                                      n_ref, C.byref(d))
+        return rc, d
+
+    def guess_batch(self, data, beg, end, n_ref):
+        p, n, dev, keep = self._ptr(data)
+        beg = np.ascontiguousarray(beg, np.int64)
+        end = np.ascontiguousarray(end, np.int64)
+        k = len(beg)
+        out = np.zeros(max(k, 1), np.int64)
+        err = np.zeros(max(k, 1), np.int32)
+        rc = self.L.hbam_guess_batch(self.h, p, dev, n, beg.ctypes.data, end.ctypes.data, k,
+                                     n_ref, out.ctypes.data, err.ctypes.data)
+        return rc, out[:k], err[:k]
+
+    def guess_bgzf_block_start(self, data, beg, end):
+        p, n, dev, keep = self._ptr(data)
+        e = C.c_int32(0)
+        r = self.L.hbam_guess_bgzf_block_start(self.h, p, dev, n, beg, end, C.byref(e))
+        return r, e.value
+
+    def probabilistic_splits(self, data, beg, end):
+        p, n, dev, keep = self._ptr(data)
+        beg = np.ascontiguousarray(beg, np.uint64)
+        end = np.ascontiguousarray(end, np.uint64)
+        k = len(beg)
+        vs = np.zeros(max(k, 1), np.uint64)
+        ve = np.zeros(max(k, 1), np.uint64)
+        r = self.L.hbam_probabilistic_splits(self.h, p, dev, n, beg.ctypes.data, end.ctypes.data,
+                                             k, vs.ctypes.data, ve.ctypes.data)
+        if r < 0:
+            return r, None, None
+        return r, vs[:r], ve[:r]

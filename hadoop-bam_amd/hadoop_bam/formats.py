@@ -1,0 +1,576 @@
+"""Host-side mirror of Hadoop-BAM's BAM input API over the MI355X C ABI.
+
+Same class names, argument meaning and error behaviour as the reference's
+org.seqdoop.hadoop_bam classes (file:line cited per class); the compute runs in
+libhbam.so on the GPU.  The Java shim in java/ binds the same C ABI.
+"""
+import io
+import os
+import struct
+
+import numpy as np
+
+from . import _lib
+
+
+# ---- exceptions (the Java classes the reference raises) ------------------------------
+class IOException(Exception):
+    pass
+
+
+class SAMFormatException(RuntimeError):
+    pass
+
+
+class FileTruncatedException(RuntimeError):
+    pass
+
+
+class RuntimeIOException(RuntimeError):
+    pass
+
+
+class RuntimeEOFException(RuntimeError):
+    pass
+
+
+class IllegalArgumentException(ValueError):
+    pass
+
+
+class JavaRuntimeException(RuntimeError):
+    """RuntimeException wrapping java.util.zip.DataFormatException."""
+
+
+_EXC = {
+    _lib.HBAM_EIO: IOException, _lib.HBAM_ETRUNC: FileTruncatedException,
+    _lib.HBAM_EFORMAT: SAMFormatException, _lib.HBAM_ERUNTIMEIO: RuntimeIOException,
+    _lib.HBAM_EEOF: RuntimeEOFException, _lib.HBAM_EREFID: IllegalArgumentException,
+    _lib.HBAM_EDATA: JavaRuntimeException,
+}
+
+
+def raise_for(code, msg=""):
+    if code == _lib.HBAM_OK:
+        return
+    exc = _EXC.get(code)
+    if exc is None:
+        raise _lib.HbamUnavailable("%s: %s" % (_lib.CODE_NAMES.get(code, code), msg))
+    raise exc(msg or _lib.CODE_NAMES.get(code, str(code)))
+
+
+# ---- Hadoop plumbing stand-ins ------------------------------------------------------
+class Configuration(dict):
+    """org.apache.hadoop.conf.Configuration (string properties)."""
+
+    def get(self, k, default=None):
+        return super().get(k, default)
+
+    def getInt(self, k, default):
+        v = self.get(k)
+        return int(v) if v is not None else default
+
+
+VALIDATION_STRINGENCY_PROPERTY = "hadoopbam.samheaderreader.validation-stringency"
+CHECK_CRC_PROPERTY = "hadoopbam.hip.check-crc"
+DEVICE_PROPERTY = "hadoopbam.hip.device"
+
+
+class FileSplit:
+    """org.apache.hadoop.mapreduce.lib.input.FileSplit."""
+
+    def __init__(self, path, start, length, hosts=()):
+        self.path, self.start, self.length, self.hosts = path, int(start), int(length), list(hosts)
+
+    def getPath(self):
+        return self.path
+
+    def getStart(self):
+        return self.start
+
+    def getLength(self):
+        return self.length
+
+    def getLocations(self):
+        return self.hosts
+
+
+def compute_file_splits(path, file_len, split_size):
+    """Hadoop 1.2.1 FileInputFormat.getSplits for one file (SPLIT_SLOP = 1.1)."""
+    out, rem = [], file_len
+    while split_size > 0 and rem / split_size > 1.1:
+        out.append(FileSplit(path, file_len - rem, split_size))
+        rem -= split_size
+    if rem:
+        out.append(FileSplit(path, file_len - rem, rem))
+    return out
+
+
+class FileVirtualSplit:
+    """FileVirtualSplit.java:38-92 — a split in BGZF virtual offsets."""
+
+    def __init__(self, path=None, v_start=0, v_end=0, locations=()):
+        self.file, self.vStart, self.vEnd = path, int(v_start), int(v_end)
+        self.locations = list(locations)
+
+    def getLocations(self):
+        return self.locations
+
+    def getLength(self):  # :64-69
+        vs_hi = self.vStart & ~0xffff
+        ve_hi = self.vEnd & ~0xffff
+        hi = ve_hi - vs_hi
+        return (self.vEnd & 0xffff) - (self.vStart & 0xffff) if hi == 0 else hi
+
+    def getPath(self):
+        return self.file
+
+    def getStartVirtualOffset(self):
+        return self.vStart
+
+    def getEndVirtualOffset(self):
+        return self.vEnd
+
+    def setStartVirtualOffset(self, vo):
+        self.vStart = int(vo)
+
+    def setEndVirtualOffset(self, vo):
+        self.vEnd = int(vo)
+
+    def write(self, out):  # :82-86  Text.writeString + two longs (big-endian)
+        b = str(self.file).encode()
+        out.write(_vlong(len(b)) + b + struct.pack(">qq", self.vStart, self.vEnd))
+
+    def readFields(self, inp):  # :87-91
+        n = _read_vlong(inp)
+        self.file = inp.read(n).decode()
+        self.vStart, self.vEnd = struct.unpack(">qq", inp.read(16))
+
+    def __eq__(self, o):
+        return (isinstance(o, FileVirtualSplit) and self.file == o.file and
+                self.vStart == o.vStart and self.vEnd == o.vEnd)
+
+    def __repr__(self):
+        return "FileVirtualSplit(%s, %#x, %#x)" % (self.file, self.vStart, self.vEnd)
+
+
+def _vlong(i):
+    """Hadoop WritableUtils.writeVLong."""
+    if -112 <= i <= 127:
+        return struct.pack("b", i)
+    ln = -112
+    if i < 0:
+        i ^= -1
+        ln = -120
+    tmp = i
+    while tmp != 0:
+        tmp >>= 8
+        ln -= 1
+    out = struct.pack("b", ln)
+    n = -(ln + 120) if ln < -120 else -(ln + 112)
+    for idx in range(n, 0, -1):
+        out += struct.pack("B", (i >> ((idx - 1) * 8)) & 0xff)
+    return out
+
+
+def _read_vlong(inp):
+    first = struct.unpack("b", inp.read(1))[0]
+    if first >= -112:
+        return first
+    neg = first < -120
+    n = -(first + 120) if neg else -(first + 112)
+    i = 0
+    for _ in range(n):
+        i = (i << 8) | inp.read(1)[0]
+    return i ^ -1 if neg else i
+
+
+# ---- device file handles -------------------------------------------------------------
+_CTX = {}
+
+
+def context(conf=None):
+    """One hbam context per (device, crc) in this process (one per Hadoop task thread)."""
+    conf = conf or Configuration()
+    dev = int(conf.get(DEVICE_PROPERTY, os.environ.get("LOCAL_RANK", 0)))
+    crc = str(conf.get(CHECK_CRC_PROPERTY, "false")).lower() == "true"
+    key = (dev, crc)
+    if key not in _CTX:
+        _CTX[key] = _lib.Context(dev, check_crc=crc, validate_refs=True)
+    return _CTX[key]
+
+
+def _read_file(path):
+    if isinstance(path, (bytes, bytearray, np.ndarray)):
+        return path
+    with open(path, "rb") as f:
+        return f.read()
+
+
+# ---- split guessers ------------------------------------------------------------------
+class BAMSplitGuesser:
+    """BAMSplitGuesser.java:50-398 (the guess runs as one device lane)."""
+
+    def __init__(self, ss, conf=None, header_stream=None):
+        self.data = _read_file(ss)
+        self.conf = conf or Configuration()
+        self.ctx = context(conf)
+        h = self.ctx.parse_header(self.data if header_stream is None else _read_file(header_stream))
+        if isinstance(h, int):
+            raise_for(h, "cannot read SAM header")
+        self.n_ref = h["n_ref"]
+        if header_stream is None and bytes(self.data[:4]) != b"\x1f\x8b\x08\x04":
+            raise SAMFormatException("Does not seem like a BAM file")
+
+    def guessNextBAMRecordStart(self, beg, end):
+        rc, out, err = self.ctx.guess_batch(self.data, [beg], [end], self.n_ref)
+        raise_for(rc, self.ctx.last_error())
+        raise_for(int(err[0]), "exception escaped the guesser")
+        return int(out[0])
+
+
+class BGZFSplitGuesser:
+    """util/BGZFSplitGuesser.java:30-148."""
+
+    def __init__(self, inp, conf=None):
+        self.data = _read_file(inp)
+        self.ctx = context(conf)
+
+    def guessNextBGZFBlockStart(self, beg, end):
+        r, e = self.ctx.guess_bgzf_block_start(self.data, beg, end)
+        raise_for(e, "exception escaped the guesser")
+        return int(r)
+
+
+class SplittingBAMIndex:
+    """SplittingBAMIndex.java:50-77 — big-endian u64 voffsets + file_len<<16."""
+
+    def __init__(self, inp=None):
+        self.offsets = []
+        if inp is not None:
+            self.readIndex(inp)
+
+    def readIndex(self, inp):
+        data = inp.read() if hasattr(inp, "read") else _read_file(inp)
+        prev = -1
+        self.offsets = []
+        for i in range(0, len(data) - 7, 8):
+            cur = struct.unpack(">q", data[i:i + 8])[0]
+            if prev > cur:
+                raise IOException("Invalid splitting BAM index; offsets not in order")
+            self.offsets.append(cur)
+            prev = cur
+        if len(self.offsets) < 2:
+            raise IOException("Invalid splitting BAM index: should contain at least 1 offset "
+                              "and the file size")
+
+    def prevAlignment(self, file_pos):
+        import bisect
+        k = bisect.bisect_right(self.offsets, file_pos << 16)
+        return self.offsets[k - 1] if k else None
+
+    def nextAlignment(self, file_pos):
+        import bisect
+        k = bisect.bisect_right(self.offsets, file_pos << 16)
+        return self.offsets[k] if k < len(self.offsets) else None
+
+    def size(self):
+        return len(self.offsets)
+
+
+# ---- record value -------------------------------------------------------------------
+class BAMRecordView:
+    """A lazily decoded BAM record (the SAMRecord the reader hands out): fixed fields
+    from the device columns, payload = the record's bytes in the inflated stream."""
+
+    __slots__ = ("_dec", "_i")
+
+    def __init__(self, dec, i):
+        self._dec, self._i = dec, i
+
+    def _c(self, k):
+        return self._dec.cols[k][self._i]
+
+    def getReferenceIndex(self):
+        return int(self._c("ref_id"))
+
+    def getAlignmentStart(self):
+        return int(np.int32(self._c("pos")) + np.int32(1))
+
+    def getFlags(self):
+        return int(self._c("flag"))
+
+    def getReadUnmappedFlag(self):
+        return bool(self.getFlags() & 4)
+
+    def getMappingQuality(self):
+        return int(self._c("mapq"))
+
+    def getMateReferenceIndex(self):
+        return int(self._c("next_ref_id"))
+
+    def getMateAlignmentStart(self):
+        return int(np.int32(self._c("next_pos")) + np.int32(1))
+
+    def getInferredInsertSize(self):
+        return int(self._c("tlen"))
+
+    def getIndexingBin(self):
+        return int(self._c("bin"))
+
+    def getReadName(self):
+        c = self._dec.cols
+        a, b = int(c["name_off"][self._i]), int(c["name_off"][self._i + 1])
+        return bytes(c["names"][a:max(a, b - 1)]).decode("latin-1")
+
+    def getCigarString(self):
+        c = self._dec.cols
+        a, b = int(c["cigar_off"][self._i]), int(c["cigar_off"][self._i + 1])
+        ops = c["cigars"][a:b]
+        if len(ops) == 0:
+            return "*"
+        return "".join("%d%s" % (int(v) >> 4, "MIDNSHP=X"[int(v) & 15]) for v in ops)
+
+    def getReadString(self):
+        c = self._dec.cols
+        a, b = int(c["seq_off"][self._i]), int(c["seq_off"][self._i + 1])
+        return bytes(c["seq"][a:b]).decode() or "*"
+
+    def getBaseQualities(self):
+        c = self._dec.cols
+        a, b = int(c["seq_off"][self._i]), int(c["seq_off"][self._i + 1])
+        return bytes(c["qual"][a:b])
+
+    def getVariableBinaryRepresentation(self):
+        return self._dec.var_block(self._i)
+
+    def toBAMBytes(self):
+        """block_size + the record (what BAMRecordCodec.encode writes for an untouched record)."""
+        return self._dec.record_bytes(self._i)
+
+
+class SAMRecordWritable:
+    """SAMRecordWritable.java:46-70."""
+
+    def __init__(self):
+        self.record = None
+
+    def get(self):
+        return self.record
+
+    def set(self, r):
+        self.record = r
+
+    def write(self, out):
+        out.write(self.record.toBAMBytes())
+
+    def readFields(self, inp):
+        bs = struct.unpack("<i", inp.read(4))[0]
+        body = inp.read(bs)
+        self.record = _StandaloneRecord(struct.pack("<i", bs) + body)
+
+
+class _StandaloneRecord:
+    def __init__(self, raw):
+        self.raw = raw
+
+    def toBAMBytes(self):
+        return self.raw
+
+    def getVariableBinaryRepresentation(self):
+        return self.raw[36:]
+
+
+class LongWritable:
+    def __init__(self, v=0):
+        self.v = int(v)
+
+    def get(self):
+        return self.v
+
+    def set(self, v):
+        self.v = int(v)
+
+
+# ---- the record reader ---------------------------------------------------------------
+class _DecodedSplit:
+    def __init__(self, cols, ubuf_host=None):
+        self.cols = cols
+        self.ubuf = ubuf_host
+
+    def var_block(self, i):
+        c = self.cols
+        if self.ubuf is not None:
+            r = int(c["rec_off"][i])
+            return bytes(self.ubuf[r + 36:r + 4 + int(c["block_size"][i])])
+        raise NotImplementedError("raw payload not downloaded")
+
+    def record_bytes(self, i):
+        r = int(self.cols["rec_off"][i])
+        return bytes(self.ubuf[r:r + 4 + int(self.cols["block_size"][i])])
+
+
+class BAMRecordReader:
+    """BAMRecordReader.java:48-188.  initialize() decodes the whole split on the GPU;
+    nextKeyValue() walks the columns and raises the reference's exception at the record
+    where the reference would raise it."""
+
+    def __init__(self):
+        self.key = LongWritable()
+        self.record = SAMRecordWritable()
+        self._init = False
+
+    @staticmethod
+    def getKey0(ref_idx, alignment_start0):
+        """(long)refIdx << 32 | alignmentStart0 — the int is sign-extended (:104-106)."""
+        v = (int(np.int32(ref_idx)) << 32) | int(np.int32(alignment_start0))
+        return ((v + (1 << 63)) % (1 << 64)) - (1 << 63)
+
+    @staticmethod
+    def getKey(ref_idx_or_record, alignment_start=None):
+        if alignment_start is not None:
+            return BAMRecordReader.getKey0(ref_idx_or_record, alignment_start - 1)
+        raise NotImplementedError("getKey(SAMRecord) is computed on the device (key column)")
+
+    def initialize(self, split, ctx=None):
+        if self._init:
+            self.close()
+        self._init = True
+        conf = ctx if isinstance(ctx, Configuration) else Configuration()
+        self.split = split
+        data = _read_file(split.getPath())
+        self.ctxt = context(conf)
+        cols = self.ctxt.decode_split(data, split.getStartVirtualOffset(),
+                                      split.getEndVirtualOffset(), n_ref=-1)
+        if cols["rc"]:
+            raise_for(cols["rc"], cols.get("error", ""))
+        if cols["n"] == 0 and cols["status"] != 0:
+            raise_for(cols["status"], "BAMRecordReader.initialize")
+        self.dec = _DecodedSplit(cols, None)
+        self._ubuf = None
+        self._data = data
+        self.i = 0
+        self.n = cols["n"]
+        self.status = cols["status"]
+        self.file_start = split.getStartVirtualOffset() >> 16
+        self.v_end = split.getEndVirtualOffset()
+
+    def _payload(self):
+        if self.dec.ubuf is None:
+            # inflated stream for SAMRecordWritable payloads (lazy: only if records are read)
+            rc, blocks = self.ctxt.scan_blocks(self._data)
+            rc2, u, off, st = self.ctxt.inflate(self._data, blocks, check_crc=False)
+            start_blk = int(np.searchsorted(blocks["coff"], self.split.getStartVirtualOffset() >> 16))
+            base = int(off[start_blk])
+            self.dec.ubuf = np.asarray(u[base:])
+        return self.dec
+
+    def nextKeyValue(self):
+        if self.i >= self.n:
+            if self.status != 0 and self.i == self.n:
+                self.i += 1
+                raise_for(self.status, "at record %d" % self.n)
+            return False
+        i = self.i
+        self.i += 1
+        self.key.set(int(self.dec.cols["key"][i]))
+        self.record.set(BAMRecordView(self._payload(), i))
+        return True
+
+    def getCurrentKey(self):
+        return self.key
+
+    def getCurrentValue(self):
+        return self.record
+
+    def getProgress(self):
+        if self.i >= self.n:
+            return 1.0
+        vp = int(self.dec.cols["voffset"][self.i])
+        file_end = self.v_end >> 16
+        return float((vp >> 16) - self.file_start) / (file_end - self.file_start + 1)
+
+    def close(self):
+        self.dec = None
+
+
+# ---- input formats -------------------------------------------------------------------
+class BAMInputFormat:
+    """BAMInputFormat.java:50-229."""
+
+    def createRecordReader(self, split, ctx=None):
+        rr = BAMRecordReader()
+        rr.initialize(split, ctx)
+        return rr
+
+    def getSplits(self, splits, cfg=None):
+        cfg = cfg or Configuration()
+        splits = sorted(splits, key=lambda s: str(s.getPath()))
+        out, i = [], 0
+        while i < len(splits):
+            try:
+                i = self._add_indexed_splits(splits, i, out, cfg)
+            except IOException:
+                i = self._add_probabilistic_splits(splits, i, out, cfg)
+        return out
+
+    def _add_indexed_splits(self, splits, i, out, cfg):  # :107-159
+        path = splits[i].getPath()
+        idx_path = str(path) + ".splitting-bai"
+        if not os.path.exists(idx_path):
+            raise IOException("no index")
+        with open(idx_path, "rb") as f:
+            idx = SplittingBAMIndex(f)
+        j_end = i
+        while j_end < len(splits) and splits[j_end].getPath() == path:
+            j_end += 1
+        pot = []
+        for j in range(i, j_end):
+            fs = splits[j]
+            start, end = fs.getStart(), fs.getStart() + fs.getLength()
+            bs = idx.nextAlignment(start)
+            be = (idx.prevAlignment(end) | 0xffff) if j == j_end - 1 else idx.nextAlignment(end)
+            if bs is None or be is None:
+                return self._add_probabilistic_splits(splits, i, out, cfg)
+            pot.append(FileVirtualSplit(path, bs, be, fs.getLocations()))
+        out.extend(pot)
+        return j_end
+
+    def _add_probabilistic_splits(self, splits, i, out, cfg):  # :163-224
+        path = splits[i].getPath()
+        data = _read_file(path)
+        ctx = context(cfg)
+        j = i
+        beg, end = [], []
+        while j < len(splits) and splits[j].getPath() == path:
+            beg.append(splits[j].getStart())
+            end.append(splits[j].getStart() + splits[j].getLength())
+            j += 1
+        n, vs, ve = ctx.probabilistic_splits(data, beg, end)
+        if n < 0:
+            raise_for(int(n), ctx.last_error())
+        for a, b in zip(vs, ve):
+            out.append(FileVirtualSplit(path, int(a), int(b), ()))
+        return j
+
+    def isSplitable(self, job=None, path=None):
+        return True
+
+
+class AnySAMInputFormat(BAMInputFormat):
+    """AnySAMInputFormat.java:52-243 — BAM by extension or the 0x1f first byte."""
+
+    TRUST_EXTS_PROPERTY = "hadoopbam.anysam.trust-exts"
+
+    def getFormat(self, path, conf=None):
+        conf = conf or Configuration()
+        trust = str(conf.get(self.TRUST_EXTS_PROPERTY, "true")).lower() != "false"
+        if trust and str(path).endswith(".bam"):
+            return "BAM"
+        with open(path, "rb") as f:
+            b = f.read(1)
+        if b == b"\x1f":
+            return "BAM"
+        if b == b"@":
+            return "SAM"
+        return None

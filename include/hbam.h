@@ -1,0 +1,187 @@
+/* hbam.h — C ABI of the MI355X-native BAM read path (libhbam.so).
+ *
+ * Drop-in boundary for Hadoop-BAM's BAM input path.  The reference's Java classes
+ * (org.seqdoop.hadoop_bam.*) keep their API and bind these entry points through
+ * Panama FFI / JNI.  Every entry point names the reference
+ * interface it replaces.  Plain C: pointers + sizes, no C++ or torch types, no
+ * exceptions across the boundary.  Negative return codes map 1:1 onto the Java
+ * exception the reference raises at the same point:
+ *
+ *   HBAM_EIO          java.io.IOException
+ *   HBAM_ETRUNC       htsjdk.samtools.FileTruncatedException
+ *   HBAM_EFORMAT      htsjdk.samtools.SAMFormatException
+ *   HBAM_ERUNTIMEIO   htsjdk.samtools.util.RuntimeIOException
+ *   HBAM_EEOF         htsjdk.samtools.util.RuntimeEOFException
+ *   HBAM_EREFID       IllegalArgumentException (reference index not in dictionary)
+ *   HBAM_EDATA        RuntimeException(java.util.zip.DataFormatException)
+ *
+ * Library-specific codes (no reference counterpart): HBAM_ENOMEM, HBAM_EUNSUPPORTED
+ * (BGZF block with ISIZE > 65536), HBAM_EDEVICE (HIP error), HBAM_EINVAL, HBAM_EMORE
+ * (the compressed window handed in ends before the split's last record).
+ *
+ * Threading: a context owns one HIP stream and is single-threaded; separate contexts
+ * (one per Hadoop task thread) are independent.  Device buffers returned in
+ * hbam_columns are owned by the context and stay valid until the next decode call on
+ * that context or hbam_release_columns().
+ */
+#ifndef HBAM_H
+#define HBAM_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HBAM_OK 0
+#define HBAM_EIO (-1)
+#define HBAM_ETRUNC (-2)
+#define HBAM_EFORMAT (-3)
+#define HBAM_ERUNTIMEIO (-4)
+#define HBAM_EEOF (-5)
+#define HBAM_EREFID (-6)
+#define HBAM_EDATA (-7)
+#define HBAM_ENOMEM (-8)
+#define HBAM_EUNSUPPORTED (-9)
+#define HBAM_EDEVICE (-10)
+#define HBAM_EINVAL (-11)
+#define HBAM_EMORE (-12)
+
+typedef struct hbam_ctx hbam_ctx;
+
+/* Configuration knobs (Hadoop Configuration properties in the Java shim):
+ *   check_crc      hadoopbam.hip.check-crc: BlockCompressedInputStream.setCheckCrcs
+ *                  (off in BAMRecordReader, on in the split guessers)
+ *   validate_refs  1 = BAMRecordCodec(header) as BAMRecordReader.java:130 builds it
+ *                  (refID / mate refID must lie in [-1, n_ref)); 0 = LazyBAMRecordFactory */
+typedef struct hbam_opts {
+  int32_t check_crc;
+  int32_t validate_refs;
+  int32_t reserved[14];
+} hbam_opts;
+
+typedef struct hbam_header {
+  int32_t l_text;
+  int32_t n_ref;           /* SAMFileHeader.getSequenceDictionary().size() */
+  uint64_t header_ulen;    /* uncompressed bytes of the BAM header */
+  uint64_t first_voffset;  /* virtual offset of the first record */
+} hbam_header;
+
+typedef struct hbam_block {
+  uint64_t coff;   /* file offset of the BGZF block */
+  uint32_t clen;   /* BSIZE + 1 */
+  uint32_t isize;  /* ISIZE footer */
+  uint32_t crc;    /* CRC32 footer */
+  uint32_t pad;
+} hbam_block;
+
+/* Decoded split, struct-of-arrays.  In hbam_decode_split's output every pointer is a
+ * device pointer owned by the context; after hbam_columns_to_host they are host
+ * pointers owned by the caller (free with hbam_free_host_columns). */
+typedef struct hbam_columns {
+  uint64_t n_records;
+  int32_t status;       /* HBAM_OK, or the exception nextKeyValue()/initialize() raises */
+  int32_t pad0;
+  uint64_t err_record;  /* record index at which `status` is raised */
+  uint64_t* voffset;    /* bci.getFilePointer() before each record */
+  int64_t* key;         /* BAMRecordReader.getKey(record) (LongWritable key) */
+  uint64_t* rec_off;    /* offset of each record's block_size field in ubuf */
+  uint8_t* ubuf;        /* inflated stream of the split (SAMRecordWritable payloads) */
+  uint64_t ubuf_len;
+  int32_t* block_size;
+  int32_t* ref_id;
+  int32_t* pos;         /* 0-based */
+  uint8_t* l_read_name;
+  uint8_t* mapq;
+  uint16_t* bin;
+  uint16_t* n_cigar;
+  uint16_t* flag;
+  int32_t* l_seq;
+  int32_t* next_ref_id;
+  int32_t* next_pos;
+  int32_t* tlen;
+  uint8_t* layout_ok;   /* 0: variable block inconsistent with the fixed lengths */
+  uint64_t* name_off;   /* n+1 offsets into names (l_read_name bytes each, incl. NUL) */
+  uint8_t* names;
+  uint64_t* cigar_off;  /* n+1 offsets (in u32 ops) into cigars */
+  uint32_t* cigars;
+  uint64_t* seq_off;    /* n+1 offsets into seq (unpacked "=ACMGRSVTWYHKDBN") and qual */
+  uint8_t* seq;
+  uint8_t* qual;
+  uint64_t* aux_off;    /* n+1 offsets into aux (raw typed tags) */
+  uint8_t* aux;
+} hbam_columns;
+
+/* Per-stage device times of the last call, milliseconds (HIP events on the context's
+ * stream), for the roofline report. */
+typedef struct hbam_timing {
+  double scan_ms, inflate_ms, crc_ms, walk_ms, decode_ms, pools_ms, total_ms;
+  uint64_t n_blocks, comp_bytes, ubuf_bytes, n_records, pool_bytes;
+} hbam_timing;
+
+/* ---- context ---------------------------------------------------------------------- */
+hbam_ctx* hbam_create(int device_ordinal, const hbam_opts* opts);
+void hbam_destroy(hbam_ctx* ctx);
+const char* hbam_last_error(const hbam_ctx* ctx);
+void* hbam_stream(hbam_ctx* ctx); /* hipStream_t of the context */
+int hbam_get_timing(const hbam_ctx* ctx, hbam_timing* out);
+
+/* ---- device staging (the Java shim maps HDFS bytes into pinned buffers) ---------- */
+int hbam_upload(hbam_ctx* ctx, const uint8_t* host, uint64_t len, uint8_t** dev_out);
+int hbam_device_free(hbam_ctx* ctx, uint8_t* dev);
+
+/* ---- SAMHeaderReader.readSAMHeaderFrom (util/SAMHeaderReader.java:53-72) ----------
+ * `file` holds the start of the BAM file (host or device per `on_device`). */
+int hbam_parse_header(hbam_ctx* ctx, const uint8_t* file, int on_device, uint64_t len,
+                      hbam_header* out);
+
+/* ---- BGZF block table: [htsjdk] BlockCompressedInputStream.readBlock framing;
+ * util/BGZFBlockIndexer.java:130-181 (skipBlock).  Chain from offset 0 of `comp`. */
+int hbam_scan_blocks(hbam_ctx* ctx, const uint8_t* comp, int on_device, uint64_t len,
+                     uint64_t base_off, hbam_block* out, uint64_t cap, uint64_t* n_out);
+
+/* ---- batched inflate: [htsjdk] BlockGunzipper.unzipBlock (JDK zlib).  Blocks are
+ * relative to `comp`; output concatenated into host `out` at out_off (n+1 entries,
+ * exclusive scan of ISIZE, filled by the call).  blk_status: 0, HBAM_EFORMAT (short
+ * output / CRC mismatch), HBAM_EDATA (DataFormatException). */
+int hbam_inflate(hbam_ctx* ctx, const uint8_t* comp, int on_device, uint64_t comp_len,
+                 const hbam_block* blks, uint64_t n, int check_crc, uint8_t* out,
+                 uint64_t out_cap, uint64_t* out_off, int32_t* blk_status);
+
+/* ---- BAMRecordReader.initialize + nextKeyValue loop (BAMRecordReader.java:108-188)
+ * over FileVirtualSplit [v_start, v_end) (FileVirtualSplit.java:38-92).
+ * `comp` = bytes [comp_base, comp_base+comp_len) of a file of length file_len.
+ * n_ref < 0: parse it from the header (comp must then start at file offset 0). */
+int hbam_decode_split(hbam_ctx* ctx, const uint8_t* comp, int on_device, uint64_t comp_base,
+                      uint64_t comp_len, uint64_t file_len, uint64_t v_start, uint64_t v_end,
+                      int32_t n_ref, hbam_columns* out);
+int hbam_columns_to_host(hbam_ctx* ctx, const hbam_columns* dev, hbam_columns* host);
+void hbam_free_host_columns(hbam_columns* host);
+void hbam_release_columns(hbam_ctx* ctx, hbam_columns* dev);
+
+/* ---- BAMSplitGuesser.guessNextBAMRecordStart (BAMSplitGuesser.java:109-212) -------
+ * Returns the virtual offset of the guessed record, or `end`.  `file` is the whole file
+ * (host or device).  *err = exception escaping the guesser (HBAM_OK normally). */
+int64_t hbam_guess_bam_record_start(hbam_ctx* ctx, const uint8_t* file, int on_device,
+                                    uint64_t file_len, int64_t beg, int64_t end, int32_t n_ref,
+                                    int32_t* err);
+/* batched guesses: k independent [beg[i], end[i]) ranges (one guesser per range). */
+int hbam_guess_batch(hbam_ctx* ctx, const uint8_t* file, int on_device, uint64_t file_len,
+                     const int64_t* beg, const int64_t* end, uint64_t k, int32_t n_ref,
+                     int64_t* out, int32_t* err);
+
+/* ---- BGZFSplitGuesser.guessNextBGZFBlockStart (util/BGZFSplitGuesser.java:51-92) --- */
+int64_t hbam_guess_bgzf_block_start(hbam_ctx* ctx, const uint8_t* file, int on_device,
+                                    uint64_t file_len, int64_t beg, int64_t end, int32_t* err);
+
+/* ---- BAMInputFormat.getSplits for one file (BAMInputFormat.java:76-103,163-224):
+ * Hadoop FileSplits [beg[i], end[i]) -> FileVirtualSplits.  Returns the number of
+ * virtual splits, or a negative code ("no reads in first split" -> HBAM_EIO). */
+int64_t hbam_probabilistic_splits(hbam_ctx* ctx, const uint8_t* file, int on_device,
+                                  uint64_t file_len, const uint64_t* beg, const uint64_t* end,
+                                  uint64_t n, uint64_t* v_start, uint64_t* v_end);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
