@@ -196,7 +196,8 @@ def main():
                    "records_per_gpu": n_rec, "parallelism": "shard%d" % args.gpus},
         "records_per_s": round(rec_all / per_step, 1),
         "stages_ms": {k: round(stage[k], 3) for k in ("scan_ms", "inflate_ms", "walk_ms",
-                                                      "decode_ms", "pools_ms", "total_ms")},
+                                                      "decode_ms", "pools_ms", "total_ms",
+                                                      "huffman_ms", "resolve_ms")},
         "roofline": {"bound": "hbm", "kernel": "k_inflate", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "algorithmic_bytes_per_launch": alg},

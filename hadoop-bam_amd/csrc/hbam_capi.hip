@@ -43,6 +43,8 @@ enum BufId {
   B_ISZ32,
   B_UBUF,
   B_LENS,
+  B_BITMAP,
+  B_TAILS,
   B_INFST,
   B_CRC,
   B_ENTRY,
@@ -147,6 +149,7 @@ int ensure(hbam_ctx* c, BufId id, size_t count, T** out) {
   return HBAM_OK;
 }
 
+float ev_ms(hbam_ctx* c, int a, int b);
 inline uint32_t grid_for(uint64_t n, uint32_t wg) { return (uint32_t)((n + wg - 1) / wg); }
 
 // stream-ordered synchronous copy (the context stream is non-blocking: a plain hipMemcpy
@@ -356,11 +359,17 @@ __global__ void k_collect_empty(const BlockRec* __restrict__ blk, const uint64_t
 int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint64_t nb,
                    const uint64_t* uoff, uint8_t* ubuf, int32_t* st, bool want_crc, uint32_t* crc) {
   uint8_t* lens;
+  uint32_t *bitmap, *tails;
   int rc;
   if ((rc = ensure(c, B_LENS, nb * LENS_SLOT, &lens))) return rc;
-  if (nb)
-    k_inflate<<<grid_for(nb, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(dcomp, blk, uoff, (uint32_t)nb,
-                                                                     ubuf, lens, st);
+  if ((rc = ensure(c, B_BITMAP, nb * BITMAP_WORDS, &bitmap))) return rc;
+  if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
+  if (nb) {
+    k_inflate_tokens<<<grid_for(nb, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
+        dcomp, blk, uoff, (uint32_t)nb, ubuf, lens, bitmap, tails, st);
+    HIPCHK(c, hipEventRecord(c->ev[11], c->stream));
+    k_resolve<<<(uint32_t)nb, 64, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, bitmap, tails, st);
+  }
   HIPCHK(c, hipGetLastError());
   if (want_crc && nb) {
     k_crc32<<<grid_for(nb, 256), 256, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, crc);
@@ -618,6 +627,8 @@ int hbam_inflate(hbam_ctx* c, const uint8_t* comp, int on_device, uint64_t comp_
   (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[1]);
   c->timing = hbam_timing{};
   c->timing.inflate_ms = ms;
+  c->timing.huffman_ms = ev_ms(c, 0, 11);
+  c->timing.resolve_ms = ev_ms(c, 11, 1);
   c->timing.n_blocks = n;
   c->timing.ubuf_bytes = uo[n];
   for (uint64_t i = 0; i < n; ++i) {
@@ -937,6 +948,8 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
 
   c->timing.scan_ms = ev_ms(c, 0, 1);
   c->timing.inflate_ms = ev_ms(c, 2, 3);
+  c->timing.huffman_ms = ev_ms(c, 2, 11);
+  c->timing.resolve_ms = ev_ms(c, 11, 3);
   c->timing.walk_ms = ev_ms(c, 4, 5);
   c->timing.decode_ms = ev_ms(c, 5, 6);
   c->timing.pools_ms = ev_ms(c, 7, 8);

@@ -130,15 +130,23 @@ __global__ void k_verify_chain(const uint8_t* __restrict__ comp, const uint64_t*
 }
 
 // ------------------------------------------------------------------------------------
-// K2: inflate, one lane per BGZF block (SIMT across blocks).  LDS: per lane 288 u16 +
-// 32 u8 symbol slots.  Block status: INF_* codes (header checks are done at scan time).
+// K2: inflate = two kernels.
+//  k_inflate_tokens (phase 1): one lane per BGZF block (SIMT across blocks); Huffman
+//    decode; literals land in ubuf, each match leaves a 3-byte descriptor in its hole and a
+//    bit in the block's match-start bitmap (TokenSink, inflate_dev.h).  LDS: per lane
+//    288 u16 + 32 u8 symbol slots.
+//  k_resolve (phase 2): one wave per block; the block's output is staged in LDS (64 KiB),
+//    matches are executed in order in batches of mutually independent copies (a match
+//    whose source ends before the first pending destination), then written back.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(INFLATE_WG) void k_inflate(const uint8_t* __restrict__ comp,
-                                                        const BlockRec* __restrict__ blk,
-                                                        const uint64_t* __restrict__ uoff,
-                                                        uint32_t nblk, uint8_t* __restrict__ ubuf,
-                                                        uint8_t* __restrict__ lens_scratch,
-                                                        int32_t* __restrict__ status) {
+__global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __restrict__ comp,
+                                                               const BlockRec* __restrict__ blk,
+                                                               const uint64_t* __restrict__ uoff,
+                                                               uint32_t nblk, uint8_t* __restrict__ ubuf,
+                                                               uint8_t* __restrict__ lens_scratch,
+                                                               uint32_t* __restrict__ bitmap,
+                                                               uint32_t* __restrict__ tails,
+                                                               int32_t* __restrict__ status) {
   __shared__ uint16_t s_ll[INFLATE_WG * 288];
   __shared__ uint8_t s_d[INFLATE_WG * 32];
   const uint32_t b = blockIdx.x * INFLATE_WG + threadIdx.x;
@@ -146,16 +154,192 @@ __global__ __launch_bounds__(INFLATE_WG) void k_inflate(const uint8_t* __restric
   const BlockRec r = blk[b];
   uint32_t produced = 0;
   int32_t st;
+  tails[2 * (uint64_t)b] = 0;
   if (r.isize > 65536u) {
     st = INF_OK;  // unsupported here; the runtime reports HBAM_EUNSUPPORTED for it
   } else if (r.clen < 26u) {
     st = INF_DATA;  // Inflater.setInput with a negative length
   } else {
-    st = inflate_raw(comp + r.coff + 18, r.clen - 26u, ubuf + uoff[b], r.isize,
-                     s_ll + threadIdx.x * 288, s_d + threadIdx.x * 32,
-                     lens_scratch + (uint64_t)b * LENS_SLOT, &produced);
+    const uint64_t u0 = uoff[b];
+    TokenSink sink;
+    sink.ubuf = ubuf;
+    sink.start = u0;
+    sink.end = u0 + r.isize;
+    sink.cur = ~0ULL;
+    sink.lo = 0;
+    sink.hi = 0;
+    sink.bm = bitmap + (uint64_t)b * BITMAP_WORDS;
+    sink.bw = 0;
+    sink.bword = 0;
+    sink.nwords = (r.isize + 31u) >> 5;
+    sink.tail = tails + 2 * (uint64_t)b;
+    st = inflate_core(comp + r.coff + 18, r.clen - 26u, r.isize, s_ll + threadIdx.x * 288,
+                      s_d + threadIdx.x * 32, lens_scratch + (uint64_t)b * LENS_SLOT, sink,
+                      &produced);
   }
   status[b] = st;
+}
+
+// Copy one match inside LDS: bytes [p, p+len) <- period-`dist` repetition of [p-dist, p).
+// All sources precede p, so the reads of a chunk are independent of its writes: issue 16
+// predicated LDS reads, then 16 writes (no per-byte read->write round trips).
+static __device__ __forceinline__ void lds_match_copy(uint8_t* o, uint32_t p, uint32_t len,
+                                                      uint32_t dist) {
+  const uint32_t src = p - dist;
+  uint32_t j = 0;  // (t mod dist) for the chunk's first byte
+  for (uint32_t t0 = 0; t0 < len; t0 += 16) {
+    uint8_t v[16];
+    uint32_t jj = j;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const uint32_t idx = dist >= len ? t0 + t : jj;
+      v[t] = (t0 + t < len) ? o[src + idx] : 0;
+      jj = (jj + 1u == dist) ? 0u : jj + 1u;
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      if (t0 + t < len) o[p + t0 + t] = v[t];
+    j = jj;
+  }
+}
+
+// LZ77 resolution of one block (phase 2).  The block is staged in LDS; its matches are
+// taken 2 KiB of output (one 64-word bitmap stretch) at a time and executed as a dataflow
+// over a 64-match window: a match runs once every byte of its source is resolved (a
+// resolved-byte bitmap in LDS: literals and finished matches), so independent matches of
+// different records run in the same round.
+__global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk,
+                                                const uint64_t* __restrict__ uoff, uint32_t nblk,
+                                                uint8_t* __restrict__ ubuf,
+                                                const uint32_t* __restrict__ bitmap,
+                                                const uint32_t* __restrict__ tails,
+                                                const int32_t* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[65536 + 32];
+  __shared__ uint32_t s_res[BITMAP_WORDS];  // resolved-byte bitmap (1 = final)
+  __shared__ uint16_t s_pos[64 * 32 / 3 + 64];
+  __shared__ uint8_t s_done[64 * 32 / 3 + 64 + 64];
+  const uint32_t b = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  if (b >= nblk) return;
+  if (status[b] != INF_OK) return;
+  const uint32_t isize = blk[b].isize;
+  if (isize == 0 || isize > 65536u) return;
+  const uint32_t* bm = bitmap + (uint64_t)b * BITMAP_WORDS;
+  const uint32_t nwords = (isize + 31u) >> 5;
+  const uint32_t tail0 = tails[2 * (uint64_t)b];
+  {
+    uint32_t any = 0;
+    for (uint32_t w = lane; w < nwords; w += 64) any |= bm[w];
+    if (!__any(any != 0) && !(tail0 & 0x80000000u)) return;
+  }
+  const uint64_t base = uoff[b];
+  const uint64_t abase = base & ~15ULL;
+  const uint32_t a0 = (uint32_t)(base - abase);
+  const uint64_t aend = base + isize;
+  const uint32_t nchunks = (uint32_t)((aend - abase + 15) >> 4);
+  for (uint32_t c = lane; c < nchunks; c += 64)
+    *(uint4*)(s_out + 16 * c) = *(const uint4*)(ubuf + abase + 16 * (uint64_t)c);
+  uint8_t* o = s_out + a0;
+  for (uint32_t w0 = 0; w0 < nwords; w0 += 64) {
+    const uint32_t word = (w0 + lane < nwords) ? bm[w0 + lane] : 0u;
+    const uint32_t cnt = __popc(word);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = __shfl_up(incl, off);
+      if ((int)lane >= off) incl += t;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    if (total == 0) continue;
+    uint32_t wpos = incl - cnt;
+    uint32_t bits = word;
+    while (bits) {
+      const uint32_t bit = __ffs(bits) - 1;
+      bits &= bits - 1;
+      s_pos[wpos] = (uint16_t)((w0 + lane) * 32 + bit);
+      s_done[wpos] = 0;
+      ++wpos;
+    }
+    // this stretch's bytes: literals resolved, match destinations not yet (bits of
+    // earlier stretches are all 1: their matches are finished)
+    s_res[w0 + lane] = 0xffffffffu;
+    __syncthreads();
+    for (uint32_t j = lane; j < total; j += 64) {
+      const uint32_t p = s_pos[j];
+      const uint32_t len = (uint32_t)o[p] + 3u;
+      for (uint32_t x = p; x < p + len;) {  // clear [p, p+len) (may run past the stretch)
+        const uint32_t wi = x >> 5, bo = x & 31u;
+        const uint32_t nb = (32u - bo) < (p + len - x) ? (32u - bo) : (p + len - x);
+        const uint32_t m = (nb == 32u ? 0xffffffffu : ((1u << nb) - 1u)) << bo;
+        atomicAnd(&s_res[wi], ~m);
+        x += nb;
+      }
+    }
+    __syncthreads();
+    for (uint32_t k = 0; k < total;) {
+      const uint32_t j = k + lane;
+      bool ready = false;
+      uint32_t p = 0, len = 0, dist = 1;
+      if (j < total && !s_done[j]) {
+        p = s_pos[j];
+        len = (uint32_t)o[p] + 3u;
+        dist = ((uint32_t)o[p + 1] | (uint32_t)o[p + 2] << 8) + 1u;
+        const uint32_t s0 = p - dist;
+        const uint32_t s1 = s0 + (len < dist ? len : dist);
+        ready = true;
+        for (uint32_t x = s0; x < s1 && ready;) {
+          const uint32_t wi = x >> 5, bo = x & 31u;
+          const uint32_t nb = (32u - bo) < (s1 - x) ? (32u - bo) : (s1 - x);
+          const uint32_t m = (nb == 32u ? 0xffffffffu : ((1u << nb) - 1u)) << bo;
+          ready = (s_res[wi] & m) == m;
+          x += nb;
+        }
+      }
+      __syncthreads();  // every lane has read its descriptor before any copy overwrites
+      if (ready) lds_match_copy(o, p, len, dist);
+      __syncthreads();
+      if (ready) {
+        s_done[j] = 1;
+        for (uint32_t x = p; x < p + len;) {
+          const uint32_t wi = x >> 5, bo = x & 31u;
+          const uint32_t nb = (32u - bo) < (p + len - x) ? (32u - bo) : (p + len - x);
+          const uint32_t m = (nb == 32u ? 0xffffffffu : ((1u << nb) - 1u)) << bo;
+          atomicOr(&s_res[wi], m);
+          x += nb;
+        }
+      }
+      __syncthreads();
+      // advance k to the first unfinished match
+      for (;;) {
+        const uint32_t q = k + lane;
+        const bool fin = (q >= total) || s_done[q];
+        const uint64_t notfin = __ballot(!fin);
+        if (notfin) {
+          k += (uint32_t)(__ffsll((unsigned long long)notfin) - 1);
+          break;
+        }
+        k += 64;
+        if (k >= total) break;
+      }
+    }
+    __syncthreads();
+  }
+  if (tail0 & 0x80000000u) {  // final match shorter than 3 bytes (output was full)
+    if (lane == 0) {
+      const uint32_t p = tail0 & 0xffffu, n = (tail0 >> 16) & 0x7fffu;
+      lds_match_copy(o, p, n, tails[2 * (uint64_t)b + 1]);
+    }
+    __syncthreads();
+  }
+  for (uint32_t c = lane; c < nchunks; c += 64) {
+    const uint64_t a = abase + 16 * (uint64_t)c;
+    if (a >= base && a + 16 <= aend) {
+      *(uint4*)(ubuf + a) = *(const uint4*)(s_out + 16 * c);
+    } else {
+      for (uint32_t t = 0; t < 16; ++t)
+        if (a + t >= base && a + t < aend) ubuf[a + t] = s_out[16 * c + t];
+    }
+  }
 }
 
 // CRC-32 (IEEE, reflected 0xEDB88320) of each inflated block, slice-by-4 tables in LDS.

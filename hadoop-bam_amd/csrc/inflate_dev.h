@@ -32,27 +32,43 @@ enum : int32_t {
 };
 
 struct BitIn {
-  const uint32_t* wp;  // next aligned word to load
+  const uint4* qp;     // next 16-byte quad to load
+  uint4 q, qn;         // current and prefetched quad
+  uint32_t qi;         // next dword of q to consume (0..4)
   uint64_t bb;         // bit buffer (LSB first)
   uint32_t bc;         // valid bits in bb
   uint32_t consumed;   // bits consumed from the stream
   uint32_t total;      // 8 * deflated bytes
 };
 
+__device__ __forceinline__ uint32_t quad_word(const uint4& q, uint32_t i) {
+  return i == 0 ? q.x : i == 1 ? q.y : i == 2 ? q.z : q.w;
+}
+// Input arrives 16 bytes per load, one quad prefetched ahead, so a refill rarely waits.
 __device__ __forceinline__ void br_init(BitIn& b, const uint8_t* p, uint32_t nbytes) {
-  const uintptr_t a = (uintptr_t)p & 3u;
-  const uint32_t* w = (const uint32_t*)(p - a);
-  const uint32_t x = __builtin_nontemporal_load(w);
-  b.bb = (uint64_t)(x >> (8u * a));
-  b.bc = 32u - 8u * (uint32_t)a;
-  b.wp = w + 1;
+  const uintptr_t a = (uintptr_t)p & 15u;
+  b.qp = (const uint4*)(p - a);
+  b.q = b.qp[0];
+  b.qn = b.qp[1];
+  b.qp += 2;
+  const uint32_t w = quad_word(b.q, (uint32_t)(a >> 2));
+  const uint32_t sh = 8u * (uint32_t)(a & 3u);
+  b.bb = (uint64_t)(w >> sh);
+  b.bc = 32u - sh;
+  b.qi = (uint32_t)(a >> 2) + 1u;
   b.consumed = 0;
   b.total = nbytes * 8u;
 }
 __device__ __forceinline__ void br_refill(BitIn& b) {
   if (b.bc <= 32u) {
-    b.bb |= (uint64_t)(*b.wp) << b.bc;
-    ++b.wp;
+    if (b.qi == 4u) {
+      b.q = b.qn;
+      b.qn = *b.qp;
+      ++b.qp;
+      b.qi = 0;
+    }
+    b.bb |= (uint64_t)quad_word(b.q, b.qi) << b.bc;
+    ++b.qi;
     b.bc += 32u;
   }
 }
@@ -168,13 +184,129 @@ __device__ __forceinline__ void dist_base(uint32_t d, uint32_t& base, uint32_t& 
   else { extra = (d >> 1) - 1u; base = ((2u + (d & 1u)) << extra) + 1u; }
 }
 
-// Inflate one raw DEFLATE stream (cdata, nbytes) to exactly isize bytes at out.
-// syms_ll: 288 u16 LDS slots; syms_d: 32 u8 LDS slots; lens: 320 B global scratch.
-// Returns INF_OK / INF_SHORT / INF_DATA; *produced = bytes written.
-__device__ int32_t inflate_raw(const uint8_t* __restrict__ cdata, uint32_t nbytes,
-                               uint8_t* __restrict__ out, uint32_t isize,
-                               uint16_t* __restrict__ syms_ll, uint8_t* __restrict__ syms_d,
-                               uint8_t* __restrict__ lens, uint32_t* produced) {
+// Output sinks.  The decoder core below is the same for both; only how symbols land in
+// memory differs.
+//
+// DirectSink: the whole block in a private buffer (guesser: BCIS needs the inflated block);
+// LZ77 copies read the lane's own output.
+struct DirectSink {
+  uint8_t* out;
+  __device__ __forceinline__ void literal(uint32_t op, uint32_t b) { out[op] = (uint8_t)b; }
+  __device__ __forceinline__ void match(uint32_t op, uint32_t n, uint32_t dist) {
+    // all sources lie in [op-dist, op): copy with period dist
+    const uint8_t* src = out + (op - dist);
+    uint8_t* dst = out + op;
+    if (dist >= n) {
+      uint32_t k = 0;
+      for (; k + 4u <= n; k += 4u) {
+        const uint8_t a0 = src[k], a1 = src[k + 1], a2 = src[k + 2], a3 = src[k + 3];
+        dst[k] = a0; dst[k + 1] = a1; dst[k + 2] = a2; dst[k + 3] = a3;
+      }
+      for (; k < n; ++k) dst[k] = src[k];
+    } else {
+      uint32_t j = 0;
+      for (uint32_t k = 0; k < n; ++k) {
+        dst[k] = src[j];
+        j = (j + 1u == dist) ? 0u : j + 1u;
+      }
+    }
+  }
+  __device__ __forceinline__ void finish(uint32_t) {}
+};
+
+// TokenSink (phase 1 of the batched inflate): literals go to their final place in ubuf;
+// each match of >= 3 bytes leaves a 3-byte descriptor (len-3, dist-1 as u8 + u16 LE) in the
+// first bytes of its destination and a bit in the block's match-start bitmap; phase 2
+// (k_resolve) fills the holes.  Stores are 16-byte chunks (register write-combining) so the
+// lane never waits on its own byte stores; only the block's first/last chunk, which it
+// shares with the neighbouring blocks, is written bytewise.
+struct TokenSink {
+  uint8_t* ubuf;
+  uint64_t start;   // absolute output offset of the block
+  uint64_t end;     // start + isize
+  uint64_t cur;     // absolute 16-byte chunk held in lo/hi (~0 = none)
+  uint64_t lo, hi;
+  uint32_t* bm;     // match-start bitmap of the block (ceil(isize/32) words)
+  uint32_t bw, bword, nwords;
+  uint32_t* tail;   // [0] = op | n<<16 | 1<<31 for a final match shorter than 3 bytes, [1] = dist
+
+  __device__ __forceinline__ void flush() {
+    if (cur == ~0ULL) return;
+    if (cur >= start && cur + 16 <= end) {
+      uint4 v;
+      v.x = (uint32_t)lo; v.y = (uint32_t)(lo >> 32); v.z = (uint32_t)hi; v.w = (uint32_t)(hi >> 32);
+      *(uint4*)(ubuf + cur) = v;
+    } else {
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint64_t a = cur + k;
+        if (a >= start && a < end) ubuf[a] = (uint8_t)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xff);
+      }
+    }
+  }
+  __device__ __forceinline__ void put(uint32_t op, uint32_t b) {
+    const uint64_t a = start + op;
+    const uint64_t c = a & ~15ULL;
+    if (c != cur) {
+      flush();
+      cur = c;
+      lo = 0;
+      hi = 0;
+    }
+    const uint32_t k = (uint32_t)(a & 15);
+    if (k < 8) lo |= (uint64_t)(b & 0xff) << (8 * k);
+    else hi |= (uint64_t)(b & 0xff) << (8 * (k - 8));
+  }
+  __device__ __forceinline__ void mark(uint32_t op) {
+    const uint32_t w = op >> 5;
+    while (bw < w) {
+      bm[bw] = bword;
+      bword = 0;
+      ++bw;
+    }
+    bword |= 1u << (op & 31);
+  }
+  __device__ __forceinline__ void literal(uint32_t op, uint32_t b) { put(op, b); }
+  __device__ __forceinline__ void match(uint32_t op, uint32_t n, uint32_t dist) {
+    if (n >= 3) {
+      // descriptor bytes (len-3, (dist-1) lo, hi) in one insert unless they cross a chunk
+      const uint32_t v = (n - 3) | (dist - 1) << 8;
+      const uint64_t a = start + op;
+      const uint32_t k = (uint32_t)(a & 15);
+      if (k <= 13 && (a & ~15ULL) == cur) {
+        if (k <= 5) lo |= (uint64_t)v << (8 * k);
+        else if (k >= 8) hi |= (uint64_t)v << (8 * (k - 8));
+        else {
+          lo |= (uint64_t)v << (8 * k);
+          hi |= (uint64_t)v >> (8 * (8 - k));
+        }
+      } else {
+        put(op, v & 0xff);
+        put(op + 1, (v >> 8) & 0xff);
+        put(op + 2, v >> 16);
+      }
+      mark(op);
+    } else {
+      tail[0] = op | n << 16 | 0x80000000u;
+      tail[1] = dist;
+    }
+  }
+  __device__ __forceinline__ void finish(uint32_t) {
+    flush();
+    while (bw < nwords) {
+      bm[bw] = bword;
+      bword = 0;
+      ++bw;
+    }
+  }
+};
+
+// Inflate one raw DEFLATE stream (cdata, nbytes) to exactly isize bytes through `sink`.
+// syms_ll: 288 u16 LDS slots; syms_d: 32 u8 LDS slots; lens: 352 B global scratch.
+// Returns INF_OK / INF_SHORT / INF_DATA; *produced = bytes accounted.
+template <typename Sink>
+__device__ int32_t inflate_core(const uint8_t* __restrict__ cdata, uint32_t nbytes, uint32_t isize,
+                                uint16_t* __restrict__ syms_ll, uint8_t* __restrict__ syms_d,
+                                uint8_t* __restrict__ lens, Sink& sink, uint32_t* produced) {
   BitIn br;
   br_init(br, cdata, nbytes);
   uint32_t op = 0;  // output position
@@ -202,7 +334,7 @@ __device__ int32_t inflate_raw(const uint8_t* __restrict__ cdata, uint32_t nbyte
         if (op == isize) goto leave;
         br_refill(br);
         if (br_avail(br) < 8u) goto leave;
-        out[op++] = (uint8_t)br.bb;
+        sink.literal(op++, (uint32_t)br.bb & 0xffu);
         br_drop(br, 8);
       }
       continue;
@@ -221,7 +353,6 @@ __device__ int32_t inflate_raw(const uint8_t* __restrict__ cdata, uint32_t nbyte
       const uint32_t ncode = ((uint32_t)(br.bb >> 10) & 15u) + 4u;
       br_drop(br, 14);
       if (nlen > 286u || ndist > 30u) { rc = INF_DATA; goto done; }
-      // code-length code lengths, permuted order
       // RFC 1951 code-length order 16,17,18,0,8,7,9,6,10,5,11,4,12,3,13,2,14,1,15
       // packed 5 bits per entry (a private array would be dynamically indexed -> scratch)
       const uint64_t ord_lo = 0x022caa324e804a30ULL, ord_hi = 0x00000003c2e1346cULL;
@@ -299,7 +430,7 @@ __device__ int32_t inflate_raw(const uint8_t* __restrict__ cdata, uint32_t nbyte
       br_drop(br, L);
       if (sym < 256u) {
         if (op == isize) goto leave;
-        out[op++] = (uint8_t)sym;
+        sink.literal(op++, sym);
         continue;
       }
       if (sym == 256u) break;  // end of block
@@ -329,23 +460,7 @@ __device__ int32_t inflate_raw(const uint8_t* __restrict__ cdata, uint32_t nbyte
       if (dist > op) { rc = INF_DATA; goto done; }
       uint32_t n = isize - op;
       n = mlen < n ? mlen : n;
-      // all sources lie in [op-dist, op): copy with period dist
-      const uint8_t* src = out + (op - dist);
-      uint8_t* dst = out + op;
-      if (dist >= n) {
-        uint32_t k = 0;
-        for (; k + 4u <= n; k += 4u) {
-          const uint8_t a0 = src[k], a1 = src[k + 1], a2 = src[k + 2], a3 = src[k + 3];
-          dst[k] = a0; dst[k + 1] = a1; dst[k + 2] = a2; dst[k + 3] = a3;
-        }
-        for (; k < n; ++k) dst[k] = src[k];
-      } else {
-        uint32_t j = 0;
-        for (uint32_t k = 0; k < n; ++k) {
-          dst[k] = src[j];
-          j = (j + 1u == dist) ? 0u : j + 1u;
-        }
-      }
+      sink.match(op, n, dist);
       op += n;
       if (n < mlen) goto leave;
     }
@@ -353,8 +468,19 @@ __device__ int32_t inflate_raw(const uint8_t* __restrict__ cdata, uint32_t nbyte
 leave:
   rc = (op == isize) ? INF_OK : INF_SHORT;
 done:
+  sink.finish(op);
   *produced = op;
   return rc;
+}
+
+// Single-pass inflate into a private buffer (used by the guesser's BCIS emulation).
+__device__ __forceinline__ int32_t inflate_raw(const uint8_t* __restrict__ cdata, uint32_t nbytes,
+                                               uint8_t* __restrict__ out, uint32_t isize,
+                                               uint16_t* __restrict__ syms_ll,
+                                               uint8_t* __restrict__ syms_d,
+                                               uint8_t* __restrict__ lens, uint32_t* produced) {
+  DirectSink s{out};
+  return inflate_core(cdata, nbytes, isize, syms_ll, syms_d, lens, s, produced);
 }
 
 }  // namespace hbam

@@ -66,7 +66,8 @@ class Block(C.Structure):
 
 class Timing(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("scan_ms", "inflate_ms", "crc_ms", "walk_ms",
-                                          "decode_ms", "pools_ms", "total_ms")] + \
+                                          "decode_ms", "pools_ms", "total_ms",
+                                          "huffman_ms", "resolve_ms")] + \
                [(n, C.c_uint64) for n in ("n_blocks", "comp_bytes", "ubuf_bytes", "n_records",
                                           "pool_bytes")]
 

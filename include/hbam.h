@@ -116,6 +116,7 @@ typedef struct hbam_columns {
  * stream), for the roofline report. */
 typedef struct hbam_timing {
   double scan_ms, inflate_ms, crc_ms, walk_ms, decode_ms, pools_ms, total_ms;
+  double huffman_ms, resolve_ms; /* inflate = k_inflate_tokens (Huffman) + k_resolve (LZ77) */
   uint64_t n_blocks, comp_bytes, ubuf_bytes, n_records, pool_bytes;
 } hbam_timing;
 
