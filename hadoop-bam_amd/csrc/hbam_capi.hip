@@ -519,7 +519,7 @@ int hbam_parse_header(hbam_ctx* c, const uint8_t* file, int on_device, uint64_t 
     uint8_t* ub;
     int32_t* st;
     if ((rc = ensure(c, B_UOFF, take + 1, &duoff))) return rc;
-    if ((rc = ensure(c, B_UBUF, uo[take] + 64, &ub))) return rc;
+    if ((rc = ensure(c, B_UBUF, uo[take] + UBUF_SLACK, &ub))) return rc;
     if ((rc = ensure(c, B_INFST, take, &st))) return rc;
     HIPCHK(c, hipMemcpyAsync(duoff, uo.data(), (take + 1) * 8, hipMemcpyHostToDevice, c->stream));
     if ((rc = inflate_blocks(c, d, blk, take, duoff, ub, st, false, nullptr))) return rc;
@@ -609,7 +609,7 @@ int hbam_inflate(hbam_ctx* c, const uint8_t* comp, int on_device, uint64_t comp_
   uint32_t* crc;
   if ((rc = ensure(c, B_BLK, n + 1, &db))) return rc;
   if ((rc = ensure(c, B_UOFF, n + 1, &duoff))) return rc;
-  if ((rc = ensure(c, B_UBUF, uo[n] + 64, &ub))) return rc;
+  if ((rc = ensure(c, B_UBUF, uo[n] + UBUF_SLACK, &ub))) return rc;
   if ((rc = ensure(c, B_INFST, n + 1, &st))) return rc;
   if ((rc = ensure(c, B_CRC, n + 1, &crc))) return rc;
   HIPCHK(c, hipMemcpyAsync(db, hb.data(), n * sizeof(BlockRec), hipMemcpyHostToDevice, c->stream));
@@ -752,7 +752,7 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   uint8_t* ub;
   int32_t* st;
   uint32_t* crc;
-  if ((rc = ensure(c, B_UBUF, utotal + 64, &ub))) return rc;
+  if ((rc = ensure(c, B_UBUF, utotal + UBUF_SLACK, &ub))) return rc;
   if ((rc = ensure(c, B_INFST, nb + 1, &st))) return rc;
   if ((rc = ensure(c, B_CRC, nb + 1, &crc))) return rc;
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
@@ -1196,3 +1196,12 @@ extern "C" int64_t hbam_probabilistic_splits(hbam_ctx* c, const uint8_t* file, i
   }
   return out;
 }
+
+#ifdef HBAM_PROF
+// Profiling build only: attach a device buffer of 16 u64 per block for the per-block cycle
+// counters of k_inflate_tokens / k_resolve (tools/profile_inflate.py --prof).
+extern "C" int hbam_prof_attach(void* dev) {
+  unsigned long long* p = (unsigned long long*)dev;
+  return hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_prof), &p, sizeof p) == hipSuccess ? 0 : -1;
+}
+#endif

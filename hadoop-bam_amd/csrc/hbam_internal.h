@@ -13,6 +13,7 @@ constexpr uint32_t LENS_SLOT = 352;     // per-block global scratch for code len
 constexpr uint32_t BITMAP_WORDS = 2048;  // per-block match-start bitmap (65536 bits)
 constexpr uint32_t WALK_CAP = 1824;     // >= 65536/36 record starts per block
 constexpr uint32_t SCAN_WG = 256;
+constexpr uint64_t UBUF_SLACK = 8192;  // k_resolve reads whole 2 KiB stretches past a block end
 constexpr uint32_t SCAN_TILE = 4096;
 constexpr uint64_t NO_ENTRY = ~0ULL;
 constexpr uint64_t CHAIN_STOP = ~0ULL - 1;

@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "inflate_dev.h"
+#include "resolve_dev.h"
 #include "hbam_internal.h"
 
 namespace hbam {
@@ -139,6 +140,13 @@ __global__ void k_verify_chain(const uint8_t* __restrict__ comp, const uint64_t*
 //    matches are executed in order in batches of mutually independent copies (a match
 //    whose source ends before the first pending destination), then written back.
 // ------------------------------------------------------------------------------------
+#ifdef HBAM_PROF
+// Profiling build only (libhbam_prof.so, tools/profile_inflate.py --prof): per-block cycle
+// counters, 16 u64 per block.
+__device__ unsigned long long* g_prof = nullptr;
+#define PROF_CLK() __builtin_amdgcn_s_memtime()
+#define PROF_RT() __builtin_amdgcn_s_memrealtime()
+#endif
 __global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __restrict__ comp,
                                                                const BlockRec* __restrict__ blk,
                                                                const uint64_t* __restrict__ uoff,
@@ -151,6 +159,9 @@ __global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __
   __shared__ uint8_t s_d[INFLATE_WG * 32];
   const uint32_t b = blockIdx.x * INFLATE_WG + threadIdx.x;
   if (b >= nblk) return;
+#ifdef HBAM_PROF
+  const uint64_t pr0 = PROF_RT(), pc0 = PROF_CLK();
+#endif
   const BlockRec r = blk[b];
   uint32_t produced = 0;
   int32_t st;
@@ -178,49 +189,34 @@ __global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __
                       &produced);
   }
   status[b] = st;
-}
-
-// Copy one match inside LDS: bytes [p, p+len) <- period-`dist` repetition of [p-dist, p).
-// All sources precede p, so the reads of a chunk are independent of its writes: issue 16
-// predicated LDS reads, then 16 writes (no per-byte read->write round trips).
-static __device__ __forceinline__ void lds_match_copy(uint8_t* o, uint32_t p, uint32_t len,
-                                                      uint32_t dist) {
-  const uint32_t src = p - dist;
-  uint32_t j = 0;  // (t mod dist) for the chunk's first byte
-  for (uint32_t t0 = 0; t0 < len; t0 += 16) {
-    uint8_t v[16];
-    uint32_t jj = j;
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const uint32_t idx = dist >= len ? t0 + t : jj;
-      v[t] = (t0 + t < len) ? o[src + idx] : 0;
-      jj = (jj + 1u == dist) ? 0u : jj + 1u;
-    }
-#pragma unroll
-    for (int t = 0; t < 16; ++t)
-      if (t0 + t < len) o[p + t0 + t] = v[t];
-    j = jj;
+#ifdef HBAM_PROF
+  if (g_prof) {
+    g_prof[16 * (uint64_t)b + 8] = pr0;
+    g_prof[16 * (uint64_t)b + 9] = PROF_RT();
+    g_prof[16 * (uint64_t)b + 10] = PROF_CLK() - pc0;
+    g_prof[16 * (uint64_t)b + 11] = produced;
   }
+#endif
 }
 
-// LZ77 resolution of one block (phase 2).  The block is staged in LDS; its matches are
-// taken 2 KiB of output (one 64-word bitmap stretch) at a time and executed as a dataflow
-// over a 64-match window: a match runs once every byte of its source is resolved (a
-// resolved-byte bitmap in LDS: literals and finished matches), so independent matches of
-// different records run in the same round.
+// LZ77 resolution of one block (phase 2 of the batched inflate); see resolve_dev.h.
 __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk,
                                                 const uint64_t* __restrict__ uoff, uint32_t nblk,
                                                 uint8_t* __restrict__ ubuf,
                                                 const uint32_t* __restrict__ bitmap,
                                                 const uint32_t* __restrict__ tails,
                                                 const int32_t* __restrict__ status) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_out[65536 + 32];
-  __shared__ uint32_t s_res[BITMAP_WORDS];  // resolved-byte bitmap (1 = final)
-  __shared__ uint16_t s_pos[64 * 32 / 3 + 64];
-  __shared__ uint8_t s_done[64 * 32 / 3 + 64 + 64];
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RS_BUF];
+  __shared__ uint64_t s_rec[RS_MAXM];   // pre matches from the front, ordered from the back
+  __shared__ uint16_t s_pos[RS_MAXM];
+  __shared__ uint64_t s_sel[8];
   const uint32_t b = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   if (b >= nblk) return;
+#ifdef HBAM_PROF
+  const uint64_t pr0 = PROF_RT(), pc0 = PROF_CLK();
+  uint64_t p_desc = 0, p_bat = 0, n_bat = 0, n_m = 0, p_st = 0;
+#endif
   if (status[b] != INF_OK) return;
   const uint32_t isize = blk[b].isize;
   if (isize == 0 || isize > 65536u) return;
@@ -232,114 +228,171 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     for (uint32_t w = lane; w < nwords; w += 64) any |= bm[w];
     if (!__any(any != 0) && !(tail0 & 0x80000000u)) return;
   }
+  if (lane < 8) {  // v_perm selectors: byte j of the period-d pattern = byte (j mod d)
+    const uint32_t d = lane ? lane : 1u;
+    uint64_t sel = 0;
+    for (uint32_t j = 0; j < 8; ++j) sel |= (uint64_t)(j % d) << (8 * j);
+    s_sel[lane] = sel;
+  }
   const uint64_t base = uoff[b];
   const uint64_t abase = base & ~15ULL;
   const uint32_t a0 = (uint32_t)(base - abase);
   const uint64_t aend = base + isize;
-  const uint32_t nchunks = (uint32_t)((aend - abase + 15) >> 4);
-  for (uint32_t c = lane; c < nchunks; c += 64)
-    *(uint4*)(s_out + 16 * c) = *(const uint4*)(ubuf + abase + 16 * (uint64_t)c);
-  uint8_t* o = s_out + a0;
-  for (uint32_t w0 = 0; w0 < nwords; w0 += 64) {
-    const uint32_t word = (w0 + lane < nwords) ? bm[w0 + lane] : 0u;
+  const uint32_t nstr = (isize + RS_S - 1) / RS_S;
+  // raw stretch k occupies global [abase + k*RS_S, +RS_S) (16-byte chunks, 2 per lane)
+  auto load_raw = [&](uint32_t k, uint4& r0, uint4& r1) {
+    const uint64_t g = abase + (uint64_t)k * RS_S + 16u * lane;
+    if (k < nstr) {
+      r0 = *(const uint4*)(ubuf + g);
+      r1 = *(const uint4*)(ubuf + g + 1024);
+    }
+  };
+  uint4 ra0 = make_uint4(0, 0, 0, 0), ra1 = ra0, rb0 = ra0, rb1 = ra0;
+  load_raw(0, ra0, ra1);
+  load_raw(1, rb0, rb1);
+  *(uint4*)(s_buf + RS_W + 16u * lane) = ra0;
+  *(uint4*)(s_buf + RS_W + 1024 + 16u * lane) = ra1;
+  *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = rb0;
+  *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = rb1;
+  load_raw(2, ra0, ra1);  // ra = raw[k+2] during stretch k
+  uint32_t wnext = (lane < nwords) ? bm[lane] : 0u;
+  __syncthreads();
+#ifdef HBAM_PROF
+  p_st = PROF_CLK() - pc0;
+#endif
+  for (uint32_t k = 0; k < nstr; ++k) {
+    const uint32_t s0 = k * RS_S;
+    const uint32_t word = wnext;
+    {
+      const uint32_t wi = (k + 1) * (RS_S / 32) + lane;
+      wnext = (k + 1 < nstr && wi < nwords) ? bm[wi] : 0u;
+    }
+    // LDS index of block offset x: x - s0 + RS_W + a0
+    const uint32_t lbase = RS_W + a0 - s0;
+#ifdef HBAM_PROF
+    const uint64_t q0 = PROF_CLK();
+#endif
+    // ---- match starts of the stretch -> s_pos (in order)
     const uint32_t cnt = __popc(word);
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t t = __shfl_up(incl, off);
-      if ((int)lane >= off) incl += t;
-    }
+    const uint32_t incl = wave_incl_sum(cnt, lane);
     const uint32_t total = __shfl(incl, 63);
-    if (total == 0) continue;
-    uint32_t wpos = incl - cnt;
-    uint32_t bits = word;
-    while (bits) {
-      const uint32_t bit = __ffs(bits) - 1;
-      bits &= bits - 1;
-      s_pos[wpos] = (uint16_t)((w0 + lane) * 32 + bit);
-      s_done[wpos] = 0;
-      ++wpos;
-    }
-    // this stretch's bytes: literals resolved, match destinations not yet (bits of
-    // earlier stretches are all 1: their matches are finished)
-    s_res[w0 + lane] = 0xffffffffu;
-    __syncthreads();
-    for (uint32_t j = lane; j < total; j += 64) {
-      const uint32_t p = s_pos[j];
-      const uint32_t len = (uint32_t)o[p] + 3u;
-      for (uint32_t x = p; x < p + len;) {  // clear [p, p+len) (may run past the stretch)
-        const uint32_t wi = x >> 5, bo = x & 31u;
-        const uint32_t nb = (32u - bo) < (p + len - x) ? (32u - bo) : (p + len - x);
-        const uint32_t m = (nb == 32u ? 0xffffffffu : ((1u << nb) - 1u)) << bo;
-        atomicAnd(&s_res[wi], ~m);
-        x += nb;
+    {
+      uint32_t wpos = incl - cnt, bits = word;
+      while (bits) {
+        const uint32_t bit = __ffs(bits) - 1;
+        bits &= bits - 1;
+        s_pos[wpos++] = (uint16_t)(s0 + 32u * lane + bit);
       }
     }
     __syncthreads();
-    for (uint32_t k = 0; k < total;) {
-      const uint32_t j = k + lane;
-      bool ready = false;
-      uint32_t p = 0, len = 0, dist = 1;
-      if (j < total && !s_done[j]) {
-        p = s_pos[j];
-        len = (uint32_t)o[p] + 3u;
-        dist = ((uint32_t)o[p + 1] | (uint32_t)o[p + 2] << 8) + 1u;
-        const uint32_t s0 = p - dist;
-        const uint32_t s1 = s0 + (len < dist ? len : dist);
-        ready = true;
-        for (uint32_t x = s0; x < s1 && ready;) {
-          const uint32_t wi = x >> 5, bo = x & 31u;
-          const uint32_t nb = (32u - bo) < (s1 - x) ? (32u - bo) : (s1 - x);
-          const uint32_t m = (nb == 32u ? 0xffffffffu : ((1u << nb) - 1u)) << bo;
-          ready = (s_res[wi] & m) == m;
-          x += nb;
-        }
+    // ---- descriptors -> records, split pre / ordered
+    uint32_t npre = 0, nord = 0;
+    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      uint64_t rec = 0;
+      bool pre = false, ord = false;
+      if (j < total) {
+        const uint32_t p = s_pos[j];
+        const uint32_t dsc = *(const uint32_t*)(s_buf + lbase + p);
+        const uint32_t len = (dsc & 0xffu) + 3u;
+        const uint32_t dist = ((dsc >> 8) & 0xffffu) + 1u;
+        const uint32_t e = p - dist + (len < dist ? len : dist);
+        rec = (uint64_t)p | (uint64_t)len << 16 | (uint64_t)dist << 32 | (uint64_t)e << 48;
+        pre = e <= s0;
+        ord = !pre;
       }
-      __syncthreads();  // every lane has read its descriptor before any copy overwrites
-      if (ready) lds_match_copy(o, p, len, dist);
-      __syncthreads();
-      if (ready) {
-        s_done[j] = 1;
-        for (uint32_t x = p; x < p + len;) {
-          const uint32_t wi = x >> 5, bo = x & 31u;
-          const uint32_t nb = (32u - bo) < (p + len - x) ? (32u - bo) : (p + len - x);
-          const uint32_t m = (nb == 32u ? 0xffffffffu : ((1u << nb) - 1u)) << bo;
-          atomicOr(&s_res[wi], m);
-          x += nb;
-        }
-      }
-      __syncthreads();
-      // advance k to the first unfinished match
-      for (;;) {
-        const uint32_t q = k + lane;
-        const bool fin = (q >= total) || s_done[q];
-        const uint64_t notfin = __ballot(!fin);
-        if (notfin) {
-          k += (uint32_t)(__ffsll((unsigned long long)notfin) - 1);
-          break;
-        }
-        k += 64;
-        if (k >= total) break;
-      }
+      const uint64_t mp = __ballot(pre), mo = __ballot(ord);
+      if (pre) s_rec[npre + lane_rank(mp)] = rec;
+      if (ord) s_rec[RS_MAXM - 1 - (nord + lane_rank(mo))] = rec;
+      npre += (uint32_t)__popcll(mp);
+      nord += (uint32_t)__popcll(mo);
     }
     __syncthreads();
-  }
-  if (tail0 & 0x80000000u) {  // final match shorter than 3 bytes (output was full)
-    if (lane == 0) {
+#ifdef HBAM_PROF
+    const uint64_t q1 = PROF_CLK();
+    p_desc += q1 - q0;
+    n_m += total;
+#endif
+    // ---- pre matches: all sources final (those older than the window were written back
+    // two stretches ago; drain this wave's stores before reading them)
+    if (s0 >= RS_W) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t j = lane; j < npre; j += 64) {
+      const uint64_t rec = s_rec[j];
+      const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
+                     dist = (uint32_t)(rec >> 32) & 0xffffu;
+      const uint32_t src = p - dist;
+      if (src + RS_W >= s0) rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
+      else rs_copy_glb(s_buf, lbase + p, len, ubuf + base + src);
+    }
+    // ---- ordered matches: in-order batches
+    for (uint32_t kk = 0; kk < nord;) {
+      const uint32_t j = kk + lane;
+      const uint64_t rec = j < nord ? s_rec[RS_MAXM - 1 - j] : ~0ULL;
+      const uint32_t pk = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rec & 0xffffu);
+      const bool ready = (j < nord) && (uint32_t)(rec >> 48) <= pk;
+      const uint64_t nr = __ballot(!ready);
+      const uint32_t c = nr ? (uint32_t)(__ffsll((unsigned long long)nr) - 1) : 64u;
+      if (lane < c) {
+        const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
+                       dist = (uint32_t)(rec >> 32) & 0xffffu;
+        rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
+      }
+      kk += c;
+#ifdef HBAM_PROF
+      ++n_bat;
+#endif
+    }
+    if ((tail0 & 0x80000000u) && (tail0 & 0xffffu) / RS_S == k && lane == 0) {
+      // final match shorter than 3 bytes (the output filled up inside it); last token
       const uint32_t p = tail0 & 0xffffu, n = (tail0 >> 16) & 0x7fffu;
-      lds_match_copy(o, p, n, tails[2 * (uint64_t)b + 1]);
+      const uint32_t d = tails[2 * (uint64_t)b + 1];
+      uint32_t jj = 0;
+      for (uint32_t t = 0; t < n; ++t) {
+        const uint32_t x = p - d + jj;
+        s_buf[lbase + p + t] = (x + RS_W >= s0) ? s_buf[lbase + x] : ubuf[base + x];
+        jj = (jj + 1u == d) ? 0u : jj + 1u;
+      }
     }
     __syncthreads();
-  }
-  for (uint32_t c = lane; c < nchunks; c += 64) {
-    const uint64_t a = abase + 16 * (uint64_t)c;
-    if (a >= base && a + 16 <= aend) {
-      *(uint4*)(ubuf + a) = *(const uint4*)(s_out + 16 * c);
-    } else {
-      for (uint32_t t = 0; t < 16; ++t)
-        if (a + t >= base && a + t < aend) ubuf[a + t] = s_out[16 * c + t];
+#ifdef HBAM_PROF
+    p_bat += PROF_CLK() - q1;
+#endif
+    // ---- write back stretch k (LDS [RS_W, RS_W + RS_S)), then slide the window by RS_S
+    // (each lane moves its own 16-byte columns, so no barrier is needed inside the move)
+#pragma unroll
+    for (uint32_t h = 0; h < RS_S / 1024; ++h) {
+      const uint4 v = *(const uint4*)(s_buf + RS_W + 1024u * h + 16u * lane);
+      const uint64_t a = abase + s0 + 1024u * h + 16u * lane;
+      if (a >= base && a + 16 <= aend) {
+        *(uint4*)(ubuf + a) = v;
+      } else if (a + 16 > base && a < aend) {
+        for (uint32_t t = 0; t < 16; ++t) {
+          const uint32_t wv = t < 4 ? v.x : t < 8 ? v.y : t < 12 ? v.z : v.w;
+          if (a + t >= base && a + t < aend) ubuf[a + t] = (uint8_t)(wv >> (8 * (t & 3)));
+        }
+      }
     }
+#pragma unroll
+    for (uint32_t i = 0; i < (RS_W + RS_S) / 1024; ++i)
+      *(uint4*)(s_buf + 1024u * i + 16u * lane) = *(const uint4*)(s_buf + RS_S + 1024u * i + 16u * lane);
+    *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = ra0;
+    *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = ra1;
+    load_raw(k + 3, ra0, ra1);
+    __syncthreads();
   }
+#ifdef HBAM_PROF
+  if (g_prof && lane == 0) {
+    unsigned long long* g = g_prof + 16 * (uint64_t)b;
+    g[0] = pr0;
+    g[1] = PROF_RT();
+    g[2] = PROF_CLK() - pc0;
+    g[3] = p_st;
+    g[4] = p_desc;
+    g[5] = p_bat;
+    g[6] = n_bat;
+    g[7] = n_m;
+  }
+#endif
 }
 
 // CRC-32 (IEEE, reflected 0xEDB88320) of each inflated block, slice-by-4 tables in LDS.

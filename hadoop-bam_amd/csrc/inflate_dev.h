@@ -268,22 +268,10 @@ struct TokenSink {
   __device__ __forceinline__ void literal(uint32_t op, uint32_t b) { put(op, b); }
   __device__ __forceinline__ void match(uint32_t op, uint32_t n, uint32_t dist) {
     if (n >= 3) {
-      // descriptor bytes (len-3, (dist-1) lo, hi) in one insert unless they cross a chunk
-      const uint32_t v = (n - 3) | (dist - 1) << 8;
-      const uint64_t a = start + op;
-      const uint32_t k = (uint32_t)(a & 15);
-      if (k <= 13 && (a & ~15ULL) == cur) {
-        if (k <= 5) lo |= (uint64_t)v << (8 * k);
-        else if (k >= 8) hi |= (uint64_t)v << (8 * (k - 8));
-        else {
-          lo |= (uint64_t)v << (8 * k);
-          hi |= (uint64_t)v >> (8 * (8 - k));
-        }
-      } else {
-        put(op, v & 0xff);
-        put(op + 1, (v >> 8) & 0xff);
-        put(op + 2, v >> 16);
-      }
+      const uint32_t d = dist - 1;
+      put(op, n - 3);
+      put(op + 1, d & 0xff);
+      put(op + 2, d >> 8);
       mark(op);
     } else {
       tail[0] = op | n << 16 | 0x80000000u;

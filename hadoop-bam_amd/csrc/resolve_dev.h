@@ -1,0 +1,121 @@
+// resolve_dev.h — LZ77 resolution (phase 2 of the batched inflate), one wave per BGZF block.
+//
+// Input (left in ubuf by k_inflate_tokens): literals at their final offsets, a 3-byte
+// descriptor (len-3, dist-1 as u8 + u16 LE) at the first bytes of every match of >= 3 bytes,
+// one bit per match start in the block's bitmap, and an optional final match of < 3 bytes
+// (`tails`).  Output: the block's inflated bytes, in place.
+//
+// The block is walked in stretches of RS_S output bytes.  LDS holds a window of the RS_W
+// bytes before the stretch, the stretch and the next stretch (matches spill up to 258 bytes
+// past their stretch), 12 KiB per wave in all, so ~11 blocks share a CU.  Per stretch:
+//   1. the stretch's match starts come from 64 bitmap words (one per lane), their
+//      descriptors are read once into an LDS record list and split into
+//        - "pre" matches: source ends before the stretch — every source byte is final —
+//          copied all in parallel, reading the window in LDS or (source older than the
+//          window, already written back) ubuf in global memory;
+//        - "ordered" matches: source ends inside the stretch; executed in order in batches,
+//          a batch = the longest prefix of the pending matches whose sources end before the
+//          first pending destination (so every source byte is final), one lane per match;
+//   2. the stretch is written back to ubuf and the window slides by RS_S.
+// Raw stretch bytes and bitmap words are prefetched two / one stretch ahead.
+#pragma once
+#include <stdint.h>
+
+namespace hbam {
+
+constexpr uint32_t RS_S = 2048;                       // stretch (output bytes)
+constexpr uint32_t RS_W = 4096;                       // window kept in LDS behind the stretch
+constexpr uint32_t RS_BUF = RS_W + 2 * RS_S + 48;     // + pad for 32-byte over-reads
+constexpr uint32_t RS_MAXM = RS_S / 3 + 2;            // matches starting in one stretch
+
+__device__ __forceinline__ uint64_t lds_rd64(const uint8_t* p) { return *(const uint64_t*)p; }
+
+// write the low n (1..8) bytes of v at p
+__device__ __forceinline__ void lds_wr_part(uint8_t* p, uint64_t v, uint32_t n) {
+  if (n >= 8) {
+    *(uint64_t*)p = v;
+    return;
+  }
+  if (n & 4u) {
+    *(uint32_t*)p = (uint32_t)v;
+    p += 4;
+    v >>= 32;
+  }
+  if (n & 2u) {
+    *(uint16_t*)p = (uint16_t)v;
+    p += 2;
+    v >>= 16;
+  }
+  if (n & 1u) *p = (uint8_t)v;
+}
+
+// 8 bytes of the period-d (1..7) sequence whose first d bytes are the low bytes of v
+__device__ __forceinline__ uint64_t periodic8(uint64_t v, uint64_t sel) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
+  const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+  return (uint64_t)r0 | (uint64_t)r1 << 32;
+}
+
+// LZ77 copy inside the LDS window: dst index di, len bytes from di - dist (sources final).
+__device__ __forceinline__ void rs_copy_lds(uint8_t* __restrict__ buf, uint32_t di, uint32_t len,
+                                            uint32_t dist, const uint64_t* __restrict__ s_sel) {
+  uint8_t* d = buf + di;
+  const uint8_t* s = buf + (di - dist);
+  if (dist < 8u) {
+    // period < 8: one 8-byte pattern, stamped every cs = d*floor(8/d) bytes
+    const uint64_t pat = periodic8(lds_rd64(s), s_sel[dist]);
+    const uint32_t cs = (dist == 3u || dist == 6u) ? 6u : (dist == 5u) ? 5u : (dist == 7u) ? 7u : 8u;
+    uint32_t t = 0;
+    for (; t + 8u <= len; t += cs) *(uint64_t*)(d + t) = pat;
+    if (t < len) lds_wr_part(d + t, pat, len - t);
+  } else if (dist >= len || dist >= 32u) {
+    // 32-byte groups: a group's sources lie before its destination
+    for (uint32_t t = 0; t < len; t += 32u) {
+      // 16-byte reads (an unaligned ds_read2_b64 pair is not used)
+      const uint4 q0 = *(const uint4*)(s + t), q1 = *(const uint4*)(s + t + 16);
+      const uint64_t v0 = q0.x | (uint64_t)q0.y << 32, v1 = q0.z | (uint64_t)q0.w << 32,
+                     v2 = q1.x | (uint64_t)q1.y << 32, v3 = q1.z | (uint64_t)q1.w << 32;
+      const uint32_t n = len - t;
+      lds_wr_part(d + t, v0, n);
+      if (n > 8u) lds_wr_part(d + t + 8, v1, n - 8u);
+      if (n > 16u) lds_wr_part(d + t + 16, v2, n - 16u);
+      if (n > 24u) lds_wr_part(d + t + 24, v3, n - 24u);
+    }
+  } else {
+    // 8 <= dist < 32, overlapping: 8-byte chunks in order
+    for (uint32_t t = 0; t < len; t += 8u) lds_wr_part(d + t, lds_rd64(s + t), len - t);
+  }
+}
+
+// copy len bytes from final global bytes g (dist > len) into the LDS window at index di
+__device__ __forceinline__ void rs_copy_glb(uint8_t* __restrict__ buf, uint32_t di, uint32_t len,
+                                            const uint8_t* __restrict__ g) {
+  uint8_t* d = buf + di;
+  for (uint32_t t = 0; t < len; t += 32u) {
+    // byte-aligned 8-byte global loads (the device runs in unaligned access mode)
+    const uint64_t v0 = *(const uint64_t*)(g + t), v1 = *(const uint64_t*)(g + t + 8),
+                   v2 = *(const uint64_t*)(g + t + 16), v3 = *(const uint64_t*)(g + t + 24);
+    const uint32_t n = len - t;
+    lds_wr_part(d + t, v0, n);
+    if (n > 8u) lds_wr_part(d + t + 8, v1, n - 8u);
+    if (n > 16u) lds_wr_part(d + t + 16, v2, n - 16u);
+    if (n > 24u) lds_wr_part(d + t + 24, v3, n - 24u);
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(x, off);
+    if ((int)lane >= off) x += t;
+  }
+  return x;
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+}  // namespace hbam

@@ -108,7 +108,7 @@ def load(path=None):
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = path or LIB_PATH
+    path = path or os.environ.get("HBAM_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise HbamUnavailable("libhbam.so not built (run __graft_entry__.build())")
     L = C.CDLL(path)

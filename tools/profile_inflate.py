@@ -16,7 +16,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=float, default=256e6)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--seed", type=int, default=2)
+ap.add_argument("--prof", action="store_true",
+                help="use libhbam_prof.so (built with -DHBAM_PROF) and print per-block cycle stats")
 a = ap.parse_args()
+if a.prof:
+    os.environ["HBAM_LIB"] = os.path.join(ROOT, "hadoop-bam_amd", "libhbam_prof.so")
 g = genbam.generate(target_bytes=int(a.size), seed=a.seed, threads=16)
 data = np.asarray(g)
 d = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
@@ -24,9 +28,42 @@ d[:len(data)].copy_(torch.from_numpy(data))
 d[len(data):].zero_()
 torch.cuda.synchronize()
 ctx = _lib.Context(0)
+if a.prof:
+    import ctypes as C
+    L = _lib.load()
+    L.hbam_prof_attach.argtypes = [C.c_void_p]
+    pbuf = torch.zeros((len(data) // 8000 + 4096) * 16, dtype=torch.int64, device="cuda")
+    assert L.hbam_prof_attach(C.c_void_p(pbuf.data_ptr())) == 0
 h = ctx.parse_header(d[:len(data)])
 for _ in range(a.reps):
     rc, cols = ctx.decode_split_device(d[:len(data)], h["first_voffset"], (len(data) << 16) | 0xffff,
                                        h["n_ref"])
     assert rc == 0 and cols.status == 0 and cols.n_records == g.n_records
     print({k: round(v, 3) if isinstance(v, float) else v for k, v in ctx.timing().items()}, flush=True)
+
+if a.prof:
+    nb = ctx.timing()["n_blocks"]
+    P = pbuf.view(-1, 16)[:nb].cpu().numpy().astype(np.float64)
+
+    def stats(name, col):
+        v = P[:, col]
+        print("  %-10s mean %10.0f  p50 %10.0f  p99 %10.0f  max %10.0f" %
+              (name, v.mean(), np.percentile(v, 50), np.percentile(v, 99), v.max()))
+
+    for lab, s0, s1, cyc in (("tokens", 8, 9, 10), ("resolve", 0, 1, 2)):
+        st, en = P[:, s0], P[:, s1]
+        ok = en > 0
+        span = (en[ok].max() - st[ok].min()) / 100.0  # s_memrealtime = 100 MHz -> us
+        busy = ((en - st)[ok]).sum() / 100.0
+        print("%s: span %.1f us, sum of block durations %.1f us, mean concurrency %.1f blocks"
+              % (lab, span, busy, busy / max(span, 1e-9)))
+        stats("cycles", cyc)
+        stats("dur_us", None) if False else None
+        d = (en - st)[ok] / 100.0
+        print("  dur_us     mean %10.2f  p50 %10.2f  p99 %10.2f  max %10.2f"
+              % (d.mean(), np.percentile(d, 50), np.percentile(d, 99), d.max()))
+    for nm, c in (("stage", 3), ("desc", 4), ("batches", 5), ("n_batch", 6), ("n_match", 7)):
+        stats(nm, c)
+    print("  cycles/batch %.1f, matches/batch %.2f" % (P[:, 5].sum() / max(P[:, 6].sum(), 1),
+                                                     P[:, 7].sum() / max(P[:, 6].sum(), 1)))
+    stats("tok_out", 11)
