@@ -87,6 +87,19 @@ enum BufId {
   B_C_SEQ,
   B_C_QUAL,
   B_C_AUX,
+  // guesser window cache
+  B_G_WORK,
+  B_G_CN,
+  B_G_CBASE,
+  B_G_SLOTS,
+  B_G_CPOS,
+  B_G_CBLK,
+  B_G_CISZ,
+  B_G_CNEFF,
+  B_G_CUOFF,
+  B_G_CUBUF,
+  B_G_CST,
+  B_G_CCRC,
   B_COUNT_ALL
 };
 
@@ -1047,7 +1060,7 @@ int guess_work(hbam_ctx* c, uint64_t k, GuessWork* w) {
   int rc;
   uint8_t* base;
   const uint64_t per = 65536 + LENS_SLOT + 8 + 8 * 3 + 4;
-  if ((rc = ensure(c, B_UBUF, k * per + 4096, &base))) return rc;
+  if ((rc = ensure(c, B_G_WORK, k * per + 4096, &base))) return rc;
   w->scratch = base;
   w->lens = base + k * 65536;
   w->bufs = w->lens + k * LENS_SLOT;
@@ -1059,6 +1072,51 @@ int guess_work(hbam_ctx* c, uint64_t k, GuessWork* w) {
   w->err = (int32_t*)(w->out + k);
   return HBAM_OK;
 }
+
+// Window block cache of a batch of guesses (see hbam_guess.hip): candidates, block records,
+// batched inflate + CRC.  Fills the GCache arrays the guess kernel reads.
+struct GuessCache {
+  uint32_t* cn = nullptr;
+  uint64_t *cbase = nullptr, *cpos = nullptr, *cuoff = nullptr;
+  BlockRec* cblk = nullptr;
+  uint8_t* cubuf = nullptr;
+  int32_t* cst = nullptr;
+  uint32_t* ccrc = nullptr;
+};
+int build_guess_cache(hbam_ctx* c, const uint8_t* d, uint64_t file_len, const int64_t* dbeg,
+                      const int64_t* dend, uint64_t k, GuessCache* gc) {
+  int rc;
+  uint64_t* slots;
+  uint32_t* cisz;
+  if ((rc = ensure(c, B_G_CN, k + 1, &gc->cn))) return rc;
+  if ((rc = ensure(c, B_G_CBASE, k + 1, &gc->cbase))) return rc;
+  if ((rc = ensure(c, B_G_SLOTS, k * GC_CAP, &slots))) return rc;
+  k_guess_cands<<<(uint32_t)k, 256, 0, c->stream>>>(d, (int64_t)file_len, dbeg, dend, gc->cn, slots);
+  HIPCHK(c, hipGetLastError());
+  // windows over the cap contribute no cached blocks: clamp the counts for the scan
+  uint32_t* cn_eff;
+  if ((rc = ensure(c, B_G_CNEFF, k + 1, &cn_eff))) return rc;
+  k_guess_clamp<<<grid_for(k, 256), 256, 0, c->stream>>>(gc->cn, (uint32_t)k, cn_eff);
+  uint64_t ncand = 0;
+  if ((rc = scan_exclusive<uint32_t>(c, cn_eff, k, gc->cbase, &ncand))) return rc;
+  if ((rc = ensure(c, B_G_CPOS, ncand + 1, &gc->cpos))) return rc;
+  if ((rc = ensure(c, B_G_CBLK, ncand + 1, &gc->cblk))) return rc;
+  if ((rc = ensure(c, B_G_CISZ, ncand + 1, &cisz))) return rc;
+  k_guess_cand_blocks<<<(uint32_t)k, 64, 0, c->stream>>>(d, (int64_t)file_len, (uint32_t)k, gc->cn,
+                                                        gc->cbase, slots, gc->cpos, gc->cblk, cisz);
+  HIPCHK(c, hipGetLastError());
+  uint64_t utotal = 0;
+  if ((rc = ensure(c, B_G_CUOFF, ncand + 1, &gc->cuoff))) return rc;
+  if ((rc = scan_exclusive<uint32_t>(c, cisz, ncand, gc->cuoff, &utotal))) return rc;
+  if ((rc = ensure(c, B_G_CUBUF, utotal + UBUF_SLACK, &gc->cubuf))) return rc;
+  if ((rc = ensure(c, B_G_CST, ncand + 1, &gc->cst))) return rc;
+  if ((rc = ensure(c, B_G_CCRC, ncand + 1, &gc->ccrc))) return rc;
+  if (ncand)
+    if ((rc = inflate_blocks(c, d, gc->cblk, ncand, gc->cuoff, gc->cubuf, gc->cst, true, gc->ccrc)))
+      return rc;
+  return HBAM_OK;
+}
+
 }  // namespace
 
 extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device, uint64_t file_len,
@@ -1070,8 +1128,6 @@ extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device,
   const uint8_t* d;
   int rc = stage_comp(c, file, on_device, file_len, &d);
   if (rc) return rc;
-  GuessWork w;
-  if ((rc = guess_work(c, k, &w))) return rc;
   // Initial ByteBuffer of BAMSplitGuesser(ss, conf): the ctor reads the file magic into it
   // (:85-87).  Only windows shorter than 4 bytes could observe a stale buffer carried over
   // from a previous guess, and those always return `end` (the XLEN seek at p0+10 fails),
@@ -1085,19 +1141,28 @@ extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device,
       memcpy(magic, c->pinned_small, n4);
     }
   }
-  std::vector<uint8_t> ib(k * 8);
-  for (uint64_t i = 0; i < k; ++i) memcpy(&ib[i * 8], magic, 8);
-  HIPCHK(c, hipMemcpyAsync(w.bufs, ib.data(), k * 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(w.beg, beg, k * 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(w.end, end, k * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipEventRecord(c->ev[9], c->stream));
-  k_guess_bam<<<grid_for(k, GUESS_WG), GUESS_WG, 0, c->stream>>>(d, (int64_t)file_len, w.beg, w.end,
-                                                                (uint32_t)k, n_ref, w.scratch, w.lens,
-                                                                w.bufs, w.out, w.err);
-  HIPCHK(c, hipGetLastError());
+  const uint64_t batch = 4096;
+  for (uint64_t g0 = 0; g0 < k; g0 += batch) {
+    const uint64_t kb = std::min(batch, k - g0);
+    GuessWork w;
+    if ((rc = guess_work(c, kb, &w))) return rc;
+    std::vector<uint8_t> ib(kb * 8);
+    for (uint64_t i = 0; i < kb; ++i) memcpy(&ib[i * 8], magic, 8);
+    HIPCHK(c, hipMemcpyAsync(w.bufs, ib.data(), kb * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(w.beg, beg + g0, kb * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(w.end, end + g0, kb * 8, hipMemcpyHostToDevice, c->stream));
+    GuessCache gc;
+    if ((rc = build_guess_cache(c, d, file_len, w.beg, w.end, kb, &gc))) return rc;
+    k_guess_bam<<<grid_for(kb, GUESS_WG), GUESS_WG, 0, c->stream>>>(
+        d, (int64_t)file_len, w.beg, w.end, (uint32_t)kb, n_ref, w.scratch, w.lens, w.bufs, w.out,
+        w.err, gc.cn, gc.cbase, gc.cpos, gc.cblk, gc.cuoff, gc.cubuf, gc.cst, gc.ccrc);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(out + g0, w.out, kb * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(err + g0, w.err, kb * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   HIPCHK(c, hipEventRecord(c->ev[10], c->stream));
-  HIPCHK(c, hipMemcpyAsync(out, w.out, k * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(err, w.err, k * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->timing = hbam_timing{};
   c->timing.total_ms = ev_ms(c, 9, 10);

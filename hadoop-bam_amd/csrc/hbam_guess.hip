@@ -12,7 +12,12 @@
 //     with CRC checking on (BAMSplitGuesser.java:130), block cache on seek;
 //   * [htsjdk] BAMRecordCodec.decode with LazyBAMRecordFactory (no refID validation);
 //   * the exception filter of :144-152 and :194-207.
-// Inflate is inflate_dev.h (zlib-exact); CRC32 is computed per inflated block.
+// Inflate + CRC32 come from a per-window block cache: before the state machines run, every
+// position of a window that carries the gzip magic is treated as a candidate block and
+// inflated by the batched two-phase inflater (k_inflate_tokens + k_resolve, zlib-exact) with
+// k_crc32, so a lane's readBlock is a binary search + a pointer, not a 64 KiB inflate.  A
+// block the cache does not hold (candidate overflow, ISIZE > 65536) is inflated in-lane
+// (inflate_dev.h, same contract).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,6 +30,19 @@ constexpr int32_t G_MAGIC = 0x04088b1f;
 constexpr int32_t G_MAGIC_SUB = 0x00024342;
 constexpr int32_t G_MAX_BYTES_READ = 3 * 0xffff + 0xfffe;
 constexpr uint32_t GUESS_WG = 64;
+constexpr uint32_t GC_CAP = 256;      // cached candidate blocks per guess window
+
+// Candidate blocks of one guess window (sorted absolute file offsets) and their inflated
+// bytes / status / CRC in the batched-inflate buffers.
+struct GCache {
+  const uint64_t* pos;   // this window's candidates (n of them)
+  uint32_t n;
+  const BlockRec* blk;   // same indexing as pos
+  const uint64_t* uoff;
+  const uint8_t* ubuf;
+  const int32_t* st;
+  const uint32_t* crc;
+};
 
 struct GStream {  // SeekableArrayStream over the window
   const uint8_t* a;
@@ -49,7 +67,10 @@ struct GBcis {
   int32_t last_len;
   int32_t cur_len;  // -1 = mCurrentBlock == null
   int32_t cur_off;
-  uint8_t* cur;     // 65536-byte global scratch
+  const uint8_t* cur;  // current block's inflated bytes (cache or scratch)
+  uint8_t* scratch;    // 65536-byte global scratch for in-lane inflates
+  int64_t wbase;       // absolute file offset of the window start
+  GCache cache;        // cache.n == 0: no cache
   uint16_t* s_ll;
   uint8_t* s_d;
   uint8_t* lens;
@@ -82,18 +103,39 @@ __device__ int32_t gb_read_block(GBcis& b, GStream& f) {
   if ((h[10] | h[11] << 8) != 6) return HBAM_EFORMAT;
   if (blen < 26) return HBAM_EDATA;
   if (isize > 65536) return HBAM_EUNSUPPORTED;
-  uint32_t produced = 0;
-  const int32_t st = inflate_raw(h + 18, (uint32_t)(blen - 26), b.cur, (uint32_t)isize, b.s_ll,
-                                 b.s_d, b.lens, &produced);
-  if (st == INF_DATA) return HBAM_EDATA;
-  if (st == INF_SHORT) return HBAM_EFORMAT;
-  if (b.check_crc) {
-    uint32_t c = 0xffffffffu;
-    for (int32_t i = 0; i < isize; ++i) c = b.crc_tab[(c ^ b.cur[i]) & 0xff] ^ (c >> 8);
-    c = ~c;
-    const uint32_t expect = (uint32_t)h[blen - 8] | (uint32_t)h[blen - 7] << 8 |
-                            (uint32_t)h[blen - 6] << 16 | (uint32_t)h[blen - 5] << 24;
-    if (c != expect) return HBAM_EFORMAT;
+  const uint32_t expect = (uint32_t)h[blen - 8] | (uint32_t)h[blen - 7] << 8 |
+                          (uint32_t)h[blen - 6] << 16 | (uint32_t)h[blen - 5] << 24;
+  // cache lookup (binary search over the window's sorted candidates)
+  int32_t hit = -1;
+  if (b.cache.n) {
+    const uint64_t want = (uint64_t)(b.wbase + P);
+    uint32_t lo = 0, hi = b.cache.n;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (b.cache.pos[mid] < want) lo = mid + 1; else hi = mid;
+    }
+    if (lo < b.cache.n && b.cache.pos[lo] == want && b.cache.blk[lo].pad &&
+        b.cache.blk[lo].clen == (uint32_t)blen && b.cache.blk[lo].isize == (uint32_t)isize)
+      hit = (int32_t)lo;
+  }
+  if (hit >= 0) {
+    const int32_t st = b.cache.st[hit];
+    if (st == INF_DATA) return HBAM_EDATA;
+    if (st == INF_SHORT) return HBAM_EFORMAT;
+    if (b.check_crc && b.cache.crc[hit] != expect) return HBAM_EFORMAT;
+    b.cur = b.cache.ubuf + b.cache.uoff[hit];
+  } else {
+    uint32_t produced = 0;
+    const int32_t st = inflate_raw(h + 18, (uint32_t)(blen - 26), b.scratch, (uint32_t)isize, b.s_ll,
+                                   b.s_d, b.lens, &produced);
+    if (st == INF_DATA) return HBAM_EDATA;
+    if (st == INF_SHORT) return HBAM_EFORMAT;
+    if (b.check_crc) {
+      uint32_t c = 0xffffffffu;
+      for (int32_t i = 0; i < isize; ++i) c = b.crc_tab[(c ^ b.scratch[i]) & 0xff] ^ (c >> 8);
+      if (~c != expect) return HBAM_EFORMAT;
+    }
+    b.cur = b.scratch;
   }
   b.cur_len = isize;
   b.cur_off = 0;
@@ -305,6 +347,7 @@ __device__ int64_t g_guess(Guesser& g, const uint8_t* file, int64_t flen, int64_
   g.in.a = file + ((beg >= 0 && beg <= flen) ? beg : 0);
   g.in.len = total;
   g.in.pos = 0;
+  g.bz.wbase = (beg >= 0 && beg <= flen) ? beg : 0;
   g.bz.block_addr = 0;
   g.bz.last_len = 0;
   g.bz.cur_len = -1;
@@ -349,6 +392,92 @@ __device__ int64_t g_guess(Guesser& g, const uint8_t* file, int64_t flen, int64_
   }
 }
 
+// Candidate blocks of each guess window: every offset of the window (the bytes
+// BAMSplitGuesser's stream can reach, :118-126) that starts with the gzip magic 1f 8b 08 04.
+// One workgroup per window; sorted by rank; count > GC_CAP marks the window uncached.
+__global__ __launch_bounds__(256) void k_guess_cands(const uint8_t* __restrict__ file, int64_t flen,
+                                                     const int64_t* __restrict__ beg,
+                                                     const int64_t* __restrict__ end,
+                                                     uint32_t* __restrict__ cn,
+                                                     uint64_t* __restrict__ cpos_slots) {
+  __shared__ uint32_t s_n;
+  __shared__ uint64_t s_p[GC_CAP];
+  const uint32_t g = blockIdx.x;
+  const int64_t b0 = beg[g];
+  int32_t want = (int32_t)(end[g] - b0);
+  if (want > G_MAX_BYTES_READ) want = G_MAX_BYTES_READ;
+  int64_t total = 0;
+  if (want > 0 && b0 >= 0 && b0 <= flen) total = (flen - b0 < want) ? flen - b0 : want;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  for (int64_t p = threadIdx.x; p + 4 <= total; p += 256) {
+    const uint8_t* q = file + b0 + p;
+    if (q[0] == 0x1f && q[1] == 0x8b && q[2] == 8 && q[3] == 4) {
+      const uint32_t k = atomicAdd(&s_n, 1u);
+      if (k < GC_CAP) s_p[k] = (uint64_t)(b0 + p);
+    }
+  }
+  __syncthreads();
+  const uint32_t n = s_n;
+  if (n > GC_CAP) {
+    if (threadIdx.x == 0) cn[g] = n;
+    return;
+  }
+  uint64_t v = 0;
+  uint32_t r = 0;
+  if (threadIdx.x < n) {
+    v = s_p[threadIdx.x];
+    for (uint32_t j = 0; j < n; ++j) r += s_p[j] < v ? 1u : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x < n) cpos_slots[(uint64_t)g * GC_CAP + r] = v;
+  if (threadIdx.x == 0) cn[g] = n;
+}
+
+__global__ void k_guess_clamp(const uint32_t* __restrict__ cn, uint32_t k, uint32_t* __restrict__ out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < k) out[g] = cn[g] <= GC_CAP ? cn[g] : 0u;
+}
+
+// Compact the per-window candidate slots and build their block records.  pad = 1 marks a
+// block the cache inflates (whole block inside the file, 26 <= BSIZE+1, ISIZE <= 65536).
+__global__ void k_guess_cand_blocks(const uint8_t* __restrict__ file, int64_t flen, uint32_t k,
+                                    const uint32_t* __restrict__ cn, const uint64_t* __restrict__ cbase,
+                                    const uint64_t* __restrict__ cpos_slots,
+                                    uint64_t* __restrict__ cpos, BlockRec* __restrict__ cblk,
+                                    uint32_t* __restrict__ cisz) {
+  const uint32_t g = blockIdx.x;
+  if (g >= k) return;
+  const uint32_t n = cn[g] <= GC_CAP ? cn[g] : 0u;
+  const uint64_t o = cbase[g];
+  for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+    const uint64_t p = cpos_slots[(uint64_t)g * GC_CAP + j];
+    BlockRec r;
+    r.coff = p;
+    r.clen = 0;
+    r.isize = 0;
+    r.crc = 0;
+    r.pad = 0;
+    if ((int64_t)p + 18 <= flen) {
+      const uint32_t bl = (uint32_t)(file[p + 16] | file[p + 17] << 8) + 1u;
+      if (bl >= 26 && (int64_t)(p + bl) <= flen) {
+        const uint8_t* f = file + p + bl - 8;
+        const uint32_t crc = (uint32_t)f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
+        const uint32_t isz = (uint32_t)f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
+        if (isz <= 65536u) {
+          r.clen = bl;
+          r.isize = isz;
+          r.crc = crc;
+          r.pad = 1;
+        }
+      }
+    }
+    cpos[o + j] = p;
+    cblk[o + j] = r;
+    cisz[o + j] = r.isize;
+  }
+}
+
 __device__ void crc_table_init(uint32_t* T) {
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     uint32_t c = i;
@@ -366,7 +495,15 @@ __global__ __launch_bounds__(GUESS_WG) void k_guess_bam(const uint8_t* __restric
                                                         uint8_t* __restrict__ lens_scratch,
                                                         uint8_t* __restrict__ bufs,
                                                         int64_t* __restrict__ out,
-                                                        int32_t* __restrict__ err) {
+                                                        int32_t* __restrict__ err,
+                                                        const uint32_t* __restrict__ cn,
+                                                        const uint64_t* __restrict__ cbase,
+                                                        const uint64_t* __restrict__ cpos,
+                                                        const BlockRec* __restrict__ cblk,
+                                                        const uint64_t* __restrict__ cuoff,
+                                                        const uint8_t* __restrict__ cubuf,
+                                                        const int32_t* __restrict__ cst,
+                                                        const uint32_t* __restrict__ ccrc) {
   __shared__ uint16_t s_ll[GUESS_WG * 288];
   __shared__ uint8_t s_d[GUESS_WG * 32];
   __shared__ uint32_t T[256];
@@ -376,7 +513,19 @@ __global__ __launch_bounds__(GUESS_WG) void k_guess_bam(const uint8_t* __restric
   Guesser g;
   g.n_ref = n_ref;
   for (int j = 0; j < 8; ++j) g.buf[j] = bufs[8 * (uint64_t)i + j];
-  g.bz.cur = scratch + (uint64_t)i * 65536;
+  g.bz.scratch = scratch + (uint64_t)i * 65536;
+  g.bz.cur = g.bz.scratch;
+  g.bz.cache.n = 0;
+  if (cn && cn[i] <= GC_CAP) {
+    const uint64_t o = cbase[i];
+    g.bz.cache.n = cn[i];
+    g.bz.cache.pos = cpos + o;
+    g.bz.cache.blk = cblk + o;
+    g.bz.cache.uoff = cuoff + o;
+    g.bz.cache.ubuf = cubuf;
+    g.bz.cache.st = cst + o;
+    g.bz.cache.crc = ccrc + o;
+  }
   g.bz.s_ll = s_ll + threadIdx.x * 288;
   g.bz.s_d = s_d + threadIdx.x * 32;
   g.bz.lens = lens_scratch + (uint64_t)i * LENS_SLOT;
@@ -413,7 +562,10 @@ __global__ __launch_bounds__(GUESS_WG) void k_guess_bgzf(const uint8_t* __restri
   bz.last_len = 0;
   bz.cur_len = -1;
   bz.cur_off = 0;
-  bz.cur = scratch + (uint64_t)i * 65536;
+  bz.scratch = scratch + (uint64_t)i * 65536;
+  bz.cur = bz.scratch;
+  bz.wbase = (b0 >= 0 && b0 <= flen) ? b0 : 0;
+  bz.cache.n = 0;
   bz.s_ll = s_ll + threadIdx.x * 288;
   bz.s_d = s_d + threadIdx.x * 32;
   bz.lens = lens_scratch + (uint64_t)i * LENS_SLOT;
