@@ -18,9 +18,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "inflate_dev.h"
-#include "resolve_dev.h"
 #include "hbam_internal.h"
+#include "inflate_dev.h"
+#include "inflate_par.h"
+#include "resolve_dev.h"
 
 namespace hbam {
 
@@ -154,11 +155,13 @@ __global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __
                                                                uint8_t* __restrict__ lens_scratch,
                                                                uint32_t* __restrict__ bitmap,
                                                                uint32_t* __restrict__ tails,
-                                                               int32_t* __restrict__ status) {
+                                                               int32_t* __restrict__ status,
+                                                               int retry_only) {
   __shared__ uint16_t s_ll[INFLATE_WG * 288];
   __shared__ uint8_t s_d[INFLATE_WG * 32];
   const uint32_t b = blockIdx.x * INFLATE_WG + threadIdx.x;
   if (b >= nblk) return;
+  if (retry_only && status[b] != INF_RETRY) return;
 #ifdef HBAM_PROF
   const uint64_t pr0 = PROF_RT(), pc0 = PROF_CLK();
 #endif
@@ -197,6 +200,46 @@ __global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __
     g_prof[16 * (uint64_t)b + 11] = produced;
   }
 #endif
+}
+
+// Phase 1, wave-parallel (inflate_par.h): one workgroup of PI_NL lanes per block.  Blocks it
+// does not finish exactly are marked INF_RETRY for k_inflate_tokens(retry_only = 1).
+__global__ __launch_bounds__(PI_NL) void k_inflate_par(const uint8_t* __restrict__ comp,
+                                                      const BlockRec* __restrict__ blk,
+                                                      const uint64_t* __restrict__ uoff, uint32_t nblk,
+                                                      uint8_t* __restrict__ ubuf,
+                                                      uint32_t* __restrict__ bitmap,
+                                                      uint32_t* __restrict__ tails,
+                                                      int32_t* __restrict__ status,
+                                                      unsigned long long* __restrict__ n_retry) {
+  __shared__ PiShared s;
+  const uint32_t b = blockIdx.x;
+  if (b >= nblk) return;
+  const BlockRec r = blk[b];
+  int32_t st;
+  PiStat ps;
+#pragma unroll
+  for (uint32_t i = 0; i < PI_NSTAT; ++i) ps.v[i] = 0;
+  if (r.isize > 65536u) {
+    st = INF_OK;  // unsupported here; the runtime reports HBAM_EUNSUPPORTED for it
+  } else if (r.clen < 26u) {
+    st = INF_DATA;  // Inflater.setInput with a negative length
+  } else {
+    st = inflate_par_block(s, comp + r.coff + 18, r.clen - 26u, r.isize, ubuf, uoff[b], ps);
+    if (st == INF_OK) {
+      const uint32_t nwords = (r.isize + 31u) >> 5;
+      uint32_t* bm = bitmap + (uint64_t)b * BITMAP_WORDS;
+      for (uint32_t i = threadIdx.x; i < nwords; i += PI_NL) bm[i] = s.bm[i];
+    }
+  }
+  if (threadIdx.x == 0) {
+    status[b] = st;
+    tails[2 * (uint64_t)b] = 0;
+    if (st == INF_RETRY) atomicAdd(n_retry, 1ull);
+    ps.v[10] = 1;
+#pragma unroll
+    for (uint32_t i = 1; i < PI_NSTAT; ++i) atomicAdd(n_retry + i, (unsigned long long)ps.v[i]);
+  }
 }
 
 // LZ77 resolution of one block (phase 2 of the batched inflate); see resolve_dev.h.

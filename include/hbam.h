@@ -57,7 +57,9 @@ typedef struct hbam_ctx hbam_ctx;
 typedef struct hbam_opts {
   int32_t check_crc;
   int32_t validate_refs;
-  int32_t reserved[14];
+  int32_t inflate_mode; /* 0 = lane-per-block Huffman pass (default, faster on MI355X);
+                           1 = wave-parallel Huffman pass with lane-per-block retry */
+  int32_t reserved[13];
 } hbam_opts;
 
 typedef struct hbam_header {
@@ -116,8 +118,10 @@ typedef struct hbam_columns {
  * stream), for the roofline report. */
 typedef struct hbam_timing {
   double scan_ms, inflate_ms, crc_ms, walk_ms, decode_ms, pools_ms, total_ms;
-  double huffman_ms, resolve_ms; /* inflate = k_inflate_tokens (Huffman) + k_resolve (LZ77) */
+  double huffman_ms, resolve_ms; /* inflate = Huffman pass (k_inflate_par [+ k_inflate_tokens
+                                    for retried blocks]) + k_resolve (LZ77) */
   uint64_t n_blocks, comp_bytes, ubuf_bytes, n_records, pool_bytes;
+  uint64_t n_retry; /* blocks the wave-parallel Huffman pass handed to the lane-per-block one */
 } hbam_timing;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -126,6 +130,11 @@ void hbam_destroy(hbam_ctx* ctx);
 const char* hbam_last_error(const hbam_ctx* ctx);
 void* hbam_stream(hbam_ctx* ctx); /* hipStream_t of the context */
 int hbam_get_timing(const hbam_ctx* ctx, hbam_timing* out);
+/* Counters of the last inflate's wave-parallel Huffman pass (diagnostics, no reference
+ * counterpart): retried blocks, rounds, DEFLATE headers, sync-failure / EOB-overflow commits,
+ * shader cycles per phase (header, pass 1, sync, plan, pass 2), blocks, active lanes, commit
+ * lanes.  Copies min(n, 13) values; returns that count. */
+int hbam_inflate_stats(hbam_ctx* ctx, uint64_t* out, uint32_t n);
 
 /* ---- device staging (the Java shim maps HDFS bytes into pinned buffers) ---------- */
 int hbam_upload(hbam_ctx* ctx, const uint8_t* host, uint64_t len, uint8_t** dev_out);

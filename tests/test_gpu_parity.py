@@ -223,3 +223,49 @@ def test_large_file_properties(gpu_ctx, genbam):
     k = got["key"][mapped & (got["ref_id"] >= 0)]
     assert np.all(np.diff(k) >= 0)
     assert got["timing"]["ubuf_bytes"] > 2 * len(data)
+
+
+# ---- wave-parallel Huffman pass (inflate_par.h) ------------------------------------------
+@pytest.mark.parametrize("kw", [dict(level=5), dict(level=6, uniform_qual=1), dict(level=1),
+                                dict(level=9), dict(payload=64, level=6), dict(level=0)])
+def test_parallel_inflate_matches_zlib_and_lane_path(gpu_ctx, oracle_mod, genbam, kw):
+    """Both Huffman passes give zlib's bytes; well-formed zlib streams never need the
+    lane-per-block retry (n_retry == 0) except where the format forces it (stored blocks are
+    handled in the fast path too)."""
+    from hadoop_bam import _lib
+    data = np.asarray(genbam.generate(records=4000, seed=33, **kw))
+    ref = oracle_mod.scan_blocks(data)
+    want = b"".join(zlib.decompressobj(-15).decompress(bytes(data[int(c) + 18:int(c) + int(l) - 8]))
+                    for c, l in zip(ref["coff"], ref["clen"]))
+    par = _lib.Context(0, inflate_mode=1)
+    rc, u, off, st = par.inflate(data, ref, check_crc=True)
+    assert rc == 0 and np.all(st == 0)
+    assert u.tobytes() == want
+    assert par.timing()["n_retry"] == 0, par.timing()
+    rc2, u2, off2, st2 = gpu_ctx.inflate(data, ref, check_crc=True)
+    assert rc2 == 0 and u2.tobytes() == want
+
+
+def test_parallel_inflate_retry_path_on_corruption(oracle_mod):
+    """Corrupted blocks go through the retry path; statuses equal the oracle's."""
+    from hadoop_bam import _lib
+    gpu_ctx = _lib.Context(0, inflate_mode=1)
+    data = _load("edge_uniform_long.bam").copy()
+    ref = oracle_mod.scan_blocks(data)
+    rng = np.random.default_rng(99)
+    nb = len(ref["coff"])
+    for i in range(0, nb, 3):
+        c, l = int(ref["coff"][i]), int(ref["clen"][i])
+        if l > 60:
+            p = c + 18 + int(rng.integers(0, l - 26))
+            data[p] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    rc, u, off, st = gpu_ctx.inflate(data, ref, check_crc=True)
+    assert rc == 0
+    assert gpu_ctx.timing()["n_retry"] > 0
+    codes = {0: 0, oracle_mod.OR_EFORMAT: -3, oracle_mod.OR_EDATA: -7}
+    for i in range(nb):
+        c, l = int(ref["coff"][i]), int(ref["clen"][i])
+        orc, out = oracle_mod.inflate_block(bytes(data[c:c + l]), check_crc=True)
+        assert int(st[i]) == codes[orc], (i, int(st[i]), orc)
+        if orc == 0:
+            assert u[int(off[i]):int(off[i + 1])].tobytes() == out
