@@ -22,6 +22,7 @@
 #include "hbam_internal.h"
 #include "hbam_kernels.hip"
 #include "hbam_guess.hip"
+#include "hbam_sort.hip"
 
 using namespace hbam;
 
@@ -100,6 +101,14 @@ enum BufId {
   B_G_CUBUF,
   B_G_CST,
   B_G_CCRC,
+  B_S_UK0,
+  B_S_UK1,
+  B_S_V0,
+  B_S_V1,
+  B_S_CNT,
+  B_S_OFF,
+  B_S_HIST,
+  B_S_LENS,
   B_COUNT_ALL
 };
 
@@ -1285,6 +1294,108 @@ extern "C" int64_t hbam_probabilistic_splits(hbam_ctx* c, const uint8_t* file, i
     }
   }
   return out;
+}
+
+// ---- Sort plugin path (Sort.java:84-188) -----------------------------
+extern "C" int hbam_sort_keys(hbam_ctx* c, const int64_t* keys, uint64_t n, int64_t* keys_out,
+                              uint32_t* perm) {
+  if (!c || (n && (!keys || !perm))) return HBAM_EINVAL;
+  if (n > 0xffffffffull) return set_err(c, HBAM_EINVAL, "hbam_sort_keys: n > 2^32-1");
+  HIPCHK(c, hipSetDevice(c->device));
+  c->timing = hbam_timing{};
+  if (n == 0) return HBAM_OK;
+  const uint32_t ntiles = (uint32_t)((n + RS_TILE - 1) / RS_TILE);
+  uint64_t *k0, *k1, *off;
+  uint32_t *v0, *v1, *cnt, *hist;
+  int rc;
+  if ((rc = ensure(c, B_S_UK0, n, &k0)) || (rc = ensure(c, B_S_UK1, n, &k1)) ||
+      (rc = ensure(c, B_S_V0, n, &v0)) || (rc = ensure(c, B_S_V1, n, &v1)) ||
+      (rc = ensure(c, B_S_CNT, (uint64_t)ntiles * 256, &cnt)) ||
+      (rc = ensure(c, B_S_OFF, (uint64_t)ntiles * 256 + 1, &off)) ||
+      (rc = ensure(c, B_S_HIST, 8 * 256, &hist)))
+    return rc;
+  HIPCHK(c, hipEventRecord(c->ev[9], c->stream));
+  HIPCHK(c, hipMemsetAsync(hist, 0, 8 * 256 * 4, c->stream));
+  const uint32_t ig = (uint32_t)std::min<uint64_t>(grid_for(n, RS_WG), 2048);
+  k_rs_init<<<ig, RS_WG, 0, c->stream>>>(keys, n, k0, v0, hist);
+  HIPCHK(c, hipGetLastError());
+  std::vector<uint32_t> h(8 * 256);
+  HIPCHK(c, copy_sync(c, h.data(), hist, h.size() * 4, hipMemcpyDeviceToHost));
+  uint64_t* kin = k0;
+  uint64_t* kout = k1;
+  uint32_t* vin = v0;
+  uint32_t* vout = v1;
+  int passes = 0;
+  for (uint32_t d = 0; d < 8; ++d) {
+    bool trivial = false;
+    for (uint32_t b = 0; b < 256; ++b) trivial |= (h[d * 256 + b] == n);
+    if (trivial) continue;  // every key has the same digit: the pass is the identity
+    const uint32_t shift = 8 * d;
+    k_rs_count<<<ntiles, RS_WG, 0, c->stream>>>(kin, n, shift, ntiles, cnt);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = scan_exclusive(c, cnt, (uint64_t)ntiles * 256, off, nullptr))) return rc;
+    k_rs_scatter<<<ntiles, RS_WG, 0, c->stream>>>(kin, vin, n, shift, ntiles, off, kout, vout);
+    HIPCHK(c, hipGetLastError());
+    std::swap(kin, kout);
+    std::swap(vin, vout);
+    ++passes;
+  }
+  HIPCHK(c, hipMemcpyAsync(perm, vin, n * 4, hipMemcpyDeviceToDevice, c->stream));
+  if (keys_out) k_rs_finish<<<grid_for(n, RS_WG), RS_WG, 0, c->stream>>>(kin, n, keys_out);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev[10], c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->timing.total_ms = ev_ms(c, 9, 10);
+  c->timing.n_records = n;
+  c->timing.n_blocks = (uint64_t)passes;  // radix passes actually run
+  return HBAM_OK;
+}
+
+extern "C" int hbam_gather_records(hbam_ctx* c, const uint8_t* ubuf, const uint64_t* rec_off,
+                                   const int32_t* block_size, const uint32_t* perm, uint64_t n,
+                                   uint8_t* out, uint64_t out_cap, uint64_t* out_off,
+                                   uint64_t* total_bytes) {
+  if (!c || !out_off || (n && !block_size) || (out && n && (!ubuf || !rec_off))) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  uint32_t* lens;
+  if ((rc = ensure(c, B_S_LENS, n + 1, &lens))) return rc;
+  HIPCHK(c, hipEventRecord(c->ev[9], c->stream));
+  if (n) k_perm_lens<<<grid_for(n, RS_WG), RS_WG, 0, c->stream>>>(block_size, perm, n, lens);
+  HIPCHK(c, hipGetLastError());
+  uint64_t tot = 0;
+  if ((rc = scan_exclusive(c, lens, n, out_off, &tot))) return rc;
+  if (total_bytes) *total_bytes = tot;
+  if (!out) return HBAM_OK;  // size query
+  if (tot > out_cap) return set_err(c, HBAM_EINVAL, "hbam_gather_records: %llu bytes > out_cap %llu",
+                                    (unsigned long long)tot, (unsigned long long)out_cap);
+  if (n) {
+    const uint64_t g = (n + RS_WG / 64 - 1) / (RS_WG / 64);
+    k_gather_records<<<(uint32_t)g, RS_WG, 0, c->stream>>>(ubuf, rec_off, perm, n, out_off, out);
+  }
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev[10], c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->timing.pools_ms = ev_ms(c, 9, 10);
+  c->timing.pool_bytes = tot;
+  return HBAM_OK;
+}
+
+extern "C" int hbam_permute(hbam_ctx* c, const void* src, uint32_t elem_size, const uint32_t* perm,
+                            uint64_t n, void* out) {
+  if (!c || (n && (!src || !perm || !out)) || (elem_size != 4 && elem_size != 8)) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (n) {
+    if (elem_size == 8)
+      k_permute<uint64_t><<<grid_for(n, RS_WG), RS_WG, 0, c->stream>>>((const uint64_t*)src, perm, n,
+                                                                        (uint64_t*)out);
+    else
+      k_permute<uint32_t><<<grid_for(n, RS_WG), RS_WG, 0, c->stream>>>((const uint32_t*)src, perm, n,
+                                                                        (uint32_t*)out);
+  }
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBAM_OK;
 }
 
 #ifdef HBAM_PROF

@@ -1,0 +1,170 @@
+// hbam_sort.hip — device side of the coordinate Sort plugin path.
+//
+// Replaces the MapReduce shuffle sort of Sort.java:84-188 (SortRecordReader keys records with
+// BAMRecordReader.getKey, Sort.java:279-295; Hadoop sorts LongWritable keys as SIGNED i64;
+// SortReducer is the identity, Sort.java:191-205).  The reference's tie order is unspecified
+// (unstable spill QuickSort + merge); this path defines it as input order, i.e. (key, file,
+// voffset), by sorting stably.
+//
+// Layout: keys are sorted as u64 with the sign bit flipped (signed order == unsigned order of
+// key ^ 1<<63), carrying a u32 record index.  LSD radix, 8-bit digits, up to 8 passes; a pass
+// whose digit is the same for every key is skipped (one fused 8-digit histogram decides, so a
+// coordinate key — refID in the high word, small — usually needs 4-5 passes).
+// Per pass: k_rs_count (per-tile digit counts, digit-major) -> exclusive scan (shared with the
+// decode path) -> k_rs_scatter (stable in-tile ranking: 64-lane ballot match per 8-bit digit,
+// cross-wave prefix through LDS, one round of 256 keys at a time so the rank follows index
+// order).  All HBM traffic is streamed: 12 B read twice + 12 B written per key per pass.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hbam {
+
+constexpr uint32_t RS_WG = 256;
+constexpr uint32_t RS_IPT = 16;
+constexpr uint32_t RS_TILE = RS_WG * RS_IPT;
+constexpr uint64_t RS_SIGN = 0x8000000000000000ull;
+
+__global__ __launch_bounds__(RS_WG) void k_rs_init(const int64_t* __restrict__ keys, uint64_t n,
+                                                   uint64_t* __restrict__ ukeys,
+                                                   uint32_t* __restrict__ idx,
+                                                   uint32_t* __restrict__ hist8) {
+  __shared__ uint32_t h[8][256];
+  for (uint32_t k = threadIdx.x; k < 8 * 256; k += RS_WG) (&h[0][0])[k] = 0;
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * RS_WG;
+  for (uint64_t i = (uint64_t)blockIdx.x * RS_WG + threadIdx.x; i < n; i += stride) {
+    const uint64_t u = (uint64_t)keys[i] ^ RS_SIGN;
+    ukeys[i] = u;
+    idx[i] = (uint32_t)i;
+#pragma unroll
+    for (uint32_t d = 0; d < 8; ++d) atomicAdd(&h[d][(u >> (8 * d)) & 255u], 1u);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < 8 * 256; k += RS_WG) {
+    const uint32_t v = (&h[0][0])[k];
+    if (v) atomicAdd(hist8 + k, v);
+  }
+}
+
+__global__ __launch_bounds__(RS_WG) void k_rs_count(const uint64_t* __restrict__ kin, uint64_t n,
+                                                    uint32_t shift, uint32_t ntiles,
+                                                    uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+  for (uint32_t r = 0; r < RS_IPT; ++r) {
+    const uint64_t i = base + r * RS_WG + threadIdx.x;
+    if (i < n) atomicAdd(&h[(kin[i] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  counts[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(RS_WG) void k_rs_scatter(const uint64_t* __restrict__ kin,
+                                                      const uint32_t* __restrict__ vin, uint64_t n,
+                                                      uint32_t shift, uint32_t ntiles,
+                                                      const uint64_t* __restrict__ off,
+                                                      uint64_t* __restrict__ kout,
+                                                      uint32_t* __restrict__ vout) {
+  __shared__ uint64_t gb[256];
+  __shared__ uint32_t run[256];
+  __shared__ uint32_t wc[RS_WG / 64][256];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  gb[tid] = off[(uint64_t)tid * ntiles + blockIdx.x];
+  run[tid] = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < RS_WG / 64; ++q) wc[q][tid] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (uint32_t r = 0; r < RS_IPT; ++r) {
+    const uint64_t i = base + r * RS_WG + tid;
+    const bool valid = i < n;
+    const uint64_t k = valid ? kin[i] : 0;
+    const uint32_t v = valid ? vin[i] : 0;
+    const uint32_t dig = (uint32_t)(k >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) {
+      const bool bit = (dig >> b) & 1u;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & lt);
+    if (valid && (peers & lt) == 0) wc[w][dig] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = run[dig] + rank;
+      for (uint32_t q = 0; q < w; ++q) pos += wc[q][dig];
+      const uint64_t dst = gb[dig] + pos;
+      kout[dst] = k;
+      vout[dst] = v;
+    }
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < RS_WG / 64; ++q) {
+      s += wc[q][tid];
+      wc[q][tid] = 0;
+    }
+    run[tid] += s;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(RS_WG) void k_rs_finish(const uint64_t* __restrict__ ukeys, uint64_t n,
+                                                     int64_t* __restrict__ keys_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * RS_WG + threadIdx.x;
+  if (i < n) keys_out[i] = (int64_t)(ukeys[i] ^ RS_SIGN);
+}
+
+template <typename T>
+__global__ __launch_bounds__(RS_WG) void k_permute(const T* __restrict__ src,
+                                                   const uint32_t* __restrict__ perm, uint64_t n,
+                                                   T* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * RS_WG + threadIdx.x;
+  if (i < n) out[i] = src[perm[i]];
+}
+
+// record payload lengths (SAMRecordWritable wire form: block_size field + record) in perm order
+__global__ __launch_bounds__(RS_WG) void k_perm_lens(const int32_t* __restrict__ block_size,
+                                                     const uint32_t* __restrict__ perm, uint64_t n,
+                                                     uint32_t* __restrict__ lens) {
+  const uint64_t i = (uint64_t)blockIdx.x * RS_WG + threadIdx.x;
+  if (i < n) lens[i] = 4u + (uint32_t)block_size[perm ? perm[i] : i];
+}
+
+// one wave per record: copy 4 + block_size bytes from ubuf[rec_off[perm[i]]] to out[out_off[i]]
+__global__ __launch_bounds__(RS_WG) void k_gather_records(const uint8_t* __restrict__ ubuf,
+                                                          const uint64_t* __restrict__ rec_off,
+                                                          const uint32_t* __restrict__ perm,
+                                                          uint64_t n,
+                                                          const uint64_t* __restrict__ out_off,
+                                                          uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * (RS_WG / 64) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t src = rec_off[perm ? perm[i] : i];
+  const uint64_t dst = out_off[i];
+  const uint32_t len = (uint32_t)(out_off[i + 1] - dst);
+  const uint8_t* s = ubuf + src;
+  uint8_t* d = out + dst;
+  if (((src ^ dst) & 3u) == 0) {
+    // co-aligned: bytes up to the first dword boundary, dwords, then the tail
+    const uint32_t head = (uint32_t)((4u - (dst & 3u)) & 3u) < len ? (uint32_t)((4u - (dst & 3u)) & 3u) : len;
+    if (lane < head) d[lane] = s[lane];
+    const uint32_t nw = (len - head) >> 2;
+    const uint32_t* s4 = (const uint32_t*)(s + head);
+    uint32_t* d4 = (uint32_t*)(d + head);
+    for (uint32_t k = lane; k < nw; k += 64) d4[k] = s4[k];
+    const uint32_t t0 = head + 4u * nw;
+    if (t0 + lane < len) d[t0 + lane] = s[t0 + lane];
+  } else {
+    for (uint32_t k = lane; k < len; k += 64) d[k] = s[k];
+  }
+}
+
+}  // namespace hbam

@@ -4,6 +4,7 @@ The product path is the HIP library only: if libhbam.so is missing or cannot cre
 device context, calls raise HbamUnavailable — there is no CPU fallback.
 """
 import ctypes as C
+import sys
 import os
 
 import numpy as np
@@ -43,6 +44,7 @@ EXPORTS = [
     "hbam_decode_split", "hbam_columns_to_host", "hbam_free_host_columns",
     "hbam_release_columns", "hbam_guess_bam_record_start", "hbam_guess_batch",
     "hbam_guess_bgzf_block_start", "hbam_probabilistic_splits",
+    "hbam_sort_keys", "hbam_gather_records", "hbam_permute",
 ]
 
 
@@ -141,6 +143,10 @@ def load(path=None):
                                                     C.c_int64, _i32p]),
         "hbam_probabilistic_splits": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, vp, vp,
                                                   C.c_uint64, vp, vp]),
+        "hbam_sort_keys": (C.c_int, [vp, vp, C.c_uint64, vp, vp]),
+        "hbam_gather_records": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, vp, C.c_uint64, vp,
+                                          C.POINTER(C.c_uint64)]),
+        "hbam_permute": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -175,6 +181,12 @@ class Context:
 
     def __init__(self, device=0, check_crc=False, validate_refs=True, inflate_mode=0):
         self.L = load()
+        # PyTorch-ROCm ships its own HIP runtime; when both live in one process, torch's must
+        # open the device first (the other order leaves torch with "No HIP GPUs").
+        if "torch" in sys.modules:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
         o = Opts()
         o.check_crc = int(check_crc)
         o.validate_refs = int(validate_refs)

@@ -191,6 +191,28 @@ int64_t hbam_probabilistic_splits(hbam_ctx* ctx, const uint8_t* file, int on_dev
                                   uint64_t file_len, const uint64_t* beg, const uint64_t* end,
                                   uint64_t n, uint64_t* v_start, uint64_t* v_end);
 
+/* ---- Sort plugin path (Sort.java:84-188, SortReducer 191-205) ------
+ * hbam_sort_keys: stable sort of n LongWritable keys (signed i64, Hadoop's comparator) on
+ * the device; replaces the MapReduce shuffle sort of Sort's map output.  Ties keep input
+ * order, so over one split's decode (voffset order) the result is ordered by (key, voffset).
+ * keys (device, i64[n]) is not modified; perm (device, u32[n]) receives the source index of
+ * each output position; keys_out (device, i64[n], may be NULL) the sorted keys.  n < 2^32.
+ * Timing: total_ms = device time, n_blocks = radix passes run. */
+int hbam_sort_keys(hbam_ctx* ctx, const int64_t* keys, uint64_t n, int64_t* keys_out,
+                   uint32_t* perm);
+/* hbam_gather_records: SAMRecordWritable.write (block_size + record bytes, SAMRecordWritable
+ * .java:62-63) of records perm[0..n) (perm NULL = identity) from an inflated stream (ubuf,
+ * rec_off, block_size: a decoded split's columns, or a received exchange buffer) into out,
+ * packed; out_off (device, u64[n+1]) gets the exclusive scan of lengths.  out == NULL: size
+ * query (total_bytes only).  All pointers device pointers except total_bytes (host). */
+int hbam_gather_records(hbam_ctx* ctx, const uint8_t* ubuf, const uint64_t* rec_off,
+                        const int32_t* block_size, const uint32_t* perm, uint64_t n, uint8_t* out,
+                        uint64_t out_cap, uint64_t* out_off, uint64_t* total_bytes);
+/* out[i] = src[perm[i]] for elem_size 4 or 8 (device pointers): carries a column (voffset,
+ * block_size) through a sort permutation. */
+int hbam_permute(hbam_ctx* ctx, const void* src, uint32_t elem_size, const uint32_t* perm,
+                 uint64_t n, void* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -198,3 +198,72 @@ def splitting_index(data, granularity=4096):
     if n < 0:
         return n
     return out[:n]
+
+
+# ---- Sort plugin path (Sort.java:84-188) --------------------------------------------------
+_REC_DT = np.dtype([("block_size", "<i4"), ("ref_id", "<i4"), ("pos", "<i4"),
+                    ("l_read_name", "u1"), ("mapq", "u1"), ("bin", "<u2"), ("n_cigar", "<u2"),
+                    ("flag", "<u2"), ("l_seq", "<i4"), ("next_ref_id", "<i4"), ("next_pos", "<i4"),
+                    ("tlen", "<i4")])
+
+
+def record_payloads(cols):
+    """SAMRecordWritable.write (SAMRecordWritable.java:62-63: BAMRecordCodec.encode of an
+    untouched lazily-decoded record = its block_size + original bytes) for every record of a
+    read_split result -> (payload uint8, offsets int64[n+1])."""
+    n = cols["n"]
+    fixed = np.zeros(n, _REC_DT)
+    for f in _REC_DT.names:
+        fixed[f] = cols[f]
+    fb = fixed.view(np.uint8).reshape(n, 36)
+    vo = cols["var_off"].astype(np.int64)
+    lens = 36 + (vo[1:] - vo[:-1])
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    out = np.zeros(int(off[-1]), np.uint8)
+    for i in range(n):
+        o = int(off[i])
+        out[o:o + 36] = fb[i]
+        out[o + 36:int(off[i + 1])] = cols["var"][int(vo[i]):int(vo[i + 1])]
+    return out, off
+
+
+def sort_order(keys):
+    """Sort's total order over LongWritable keys (signed i64 comparator, Sort.java:149-157 +
+    TotalOrderPartitioner; identity reduce).  The reference leaves ties unspecified; the
+    documented order is input order (key, file, voffset): a stable sort."""
+    return np.argsort(np.asarray(keys, np.int64), kind="stable")
+
+
+class CpuSortOps:
+    """The Sort exchange's local ops on CPU tensors, restated with numpy (tests' gloo runs)."""
+
+    @staticmethod
+    def run_from_arrays(keys, voffset, block_size, payload, offsets):
+        import torch
+        o = sort_order(keys)
+        new_off, pay = _regather(payload, offsets, o)
+        from hadoop_bam.sort import SortedRun
+        return SortedRun(torch.from_numpy(np.asarray(keys, np.int64)[o].copy()),
+                         torch.from_numpy(np.asarray(voffset).astype(np.int64)[o].copy()),
+                         torch.from_numpy(np.asarray(block_size, np.int32)[o].copy()),
+                         torch.from_numpy(pay), torch.from_numpy(new_off))
+
+    @staticmethod
+    def sort_received(keys, voffset, block_size, payload):
+        bs = block_size.numpy().astype(np.int64)
+        off = np.zeros(len(bs) + 1, np.int64)
+        off[1:] = np.cumsum(4 + bs)
+        return CpuSortOps.run_from_arrays(keys.numpy(), voffset.numpy(), block_size.numpy(),
+                                          payload.numpy(), off)
+
+
+def _regather(payload, offsets, order):
+    offsets = np.asarray(offsets, np.int64)
+    lens = (offsets[1:] - offsets[:-1])[order]
+    new_off = np.zeros(len(order) + 1, np.int64)
+    new_off[1:] = np.cumsum(lens)
+    out = np.zeros(int(new_off[-1]), np.uint8)
+    for j, i in enumerate(order):
+        out[new_off[j]:new_off[j + 1]] = payload[offsets[i]:offsets[i + 1]]
+    return new_off, out

@@ -47,6 +47,7 @@ SMALL_PE_PARAMS = dict(records=20000, seed=1, odd_every=211, long_every=7919,
 
 @pytest.fixture(scope="session")
 def gpu_ctx():
+    import torch  # noqa: F401  (its HIP runtime opens the device before libhbam's)
     from hadoop_bam import _lib
     try:
         return _lib.Context(0)

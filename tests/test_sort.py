@@ -1,0 +1,174 @@
+"""Coordinate Sort plugin path (Sort.java:84-188).
+
+CPU (gloo, world size 2): the exchange — split points, all_to_all by key range, local stable
+sort — with the oracle's numpy sort as the local op; the concatenation over ranks must equal
+the oracle's total order over the whole file (key, then voffset), payload bytes included.
+GPU: hbam_sort_keys against numpy's stable argsort (negative keys, ties, unmapped-hash keys,
+skipped passes), hbam_gather_records / hbam_permute, and the single-GPU decode -> sort path
+against the oracle on the same files.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_sorted(data):
+    import oracle
+    h = oracle.read_header(data)
+    cols = oracle.read_split(data, h["first_voffset"], (len(data) << 16) | 0xffff)
+    pay, off = oracle.record_payloads(cols)
+    o = oracle.sort_order(cols["key"])
+    new_off, new_pay = oracle._regather(pay, off, o)
+    return cols["key"][o], cols["voffset"].astype(np.int64)[o], new_pay, new_off, cols
+
+
+def _sort_worker(rank, world, port, fname, out_q):
+    sys.path[:0] = [os.path.join(ROOT, "hadoop-bam_amd"), os.path.join(ROOT, "oracle")]
+    import torch.distributed as dist
+    import oracle
+    from hadoop_bam import parallel, sort
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    data = np.fromfile(os.path.join(GOLDEN, fname), dtype=np.uint8)
+    # byte-range shards: FileSplits [k*C/P, (k+1)*C/P) aligned by the guesser (a-8/a-10)
+    b = np.array([len(data) * k // world for k in range(world)], np.uint64)
+    e = np.array([len(data) * (k + 1) // world for k in range(world)], np.uint64)
+    vs, ve = oracle.probabilistic_splits(data, b, e)
+    cols = oracle.read_split(data, int(vs[rank]), int(ve[rank])) if rank < len(vs) else None
+    if cols is not None and cols["n"]:
+        pay, off = oracle.record_payloads(cols)
+        run = oracle.CpuSortOps.run_from_arrays(cols["key"], cols["voffset"], cols["block_size"],
+                                                pay, off)
+    else:
+        import torch
+        run = sort.SortedRun(torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64),
+                             torch.zeros(0, dtype=torch.int32), torch.zeros(0, dtype=torch.uint8),
+                             torch.zeros(1, dtype=torch.int64))
+    out = sort.sort_sharded(run, dist, oracle.CpuSortOps, parallel.torch_all_gather_fn(dist, "cpu"))
+    out_q.put((rank, out.keys.numpy().tolist(), out.voffset.numpy().tolist(),
+               out.payload.numpy().tobytes()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fname", ["edge_unsorted_l1.bam", "small_pe.bam"])
+def test_two_rank_sort_matches_total_order(oracle_mod, fname):
+    import torch.multiprocessing as mp
+    data = np.fromfile(os.path.join(GOLDEN, fname), dtype=np.uint8)
+    want_k, want_v, want_p, _, _ = _oracle_sorted(data)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sort_worker, args=(r, 2, port, fname, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    keys = np.concatenate([np.array(r[1], np.int64) for r in res])
+    vo = np.concatenate([np.array(r[2], np.int64) for r in res])
+    pay = b"".join(r[3] for r in res)
+    assert np.array_equal(keys, want_k)
+    assert np.array_equal(vo, want_v)
+    assert pay == want_p.tobytes()
+    assert len(res[0][1]) > 0 and len(res[1][1]) > 0  # both partitions non-empty
+
+
+def test_oracle_payload_is_record_bytes(oracle_mod):
+    """record_payloads reproduces the inflated record stream byte for byte."""
+    import zlib
+    data = np.fromfile(os.path.join(GOLDEN, "small_pe.bam"), dtype=np.uint8)
+    blocks = oracle_mod.scan_blocks(data)
+    u = b"".join(zlib.decompressobj(-15).decompress(bytes(data[int(c) + 18:int(c) + int(l) - 8]))
+                 for c, l in zip(blocks["coff"], blocks["clen"]))
+    h = oracle_mod.read_header(data)
+    cols = oracle_mod.read_split(data, h["first_voffset"], (len(data) << 16) | 0xffff)
+    pay, off = oracle_mod.record_payloads(cols)
+    start = h["header_ulen"]
+    assert pay.tobytes() == u[start:start + len(pay)]
+
+
+# ---- GPU -------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,kind", [(0, "rand"), (1, "rand"), (4095, "rand"), (4097, "dups"),
+                                    (300001, "rand"), (1 << 20, "coord"), (200000, "const")])
+def test_device_radix_sort_is_stable_signed(gpu_ctx, n, kind):
+    import torch
+    from hadoop_bam import sort
+    rng = np.random.default_rng(n + 7)
+    if kind == "rand":
+        k = rng.integers(-(1 << 63), (1 << 63) - 1, n, dtype=np.int64)
+    elif kind == "dups":
+        k = rng.integers(-3, 3, n).astype(np.int64)
+    elif kind == "coord":  # refID<<32 | pos, plus unmapped (0x7fffffff<<32 | hash) incl. negative
+        ref = rng.integers(-1, 25, n).astype(np.int64)
+        pos = rng.integers(-1, 250_000_000, n).astype(np.int64)
+        k = (ref << 32) | (pos & 0xffffffff)
+        um = rng.random(n) < 0.05
+        h = rng.integers(-(1 << 31), 1 << 31, n).astype(np.int64)
+        k[um] = (np.int64(0x7fffffff) << 32) | (h[um] & 0xffffffff)
+        k[um & (h < 0)] = h[um & (h < 0)]  # sign-extended (BAMRecordReader.java:92-95)
+    else:
+        k = np.full(n, 42, np.int64)
+    ops = sort.HipSortOps(gpu_ctx)
+    d = torch.from_numpy(k).cuda()
+    keys_s, perm = ops._sort(d.data_ptr(), n)
+    want = np.argsort(k, kind="stable")
+    assert np.array_equal(perm[:n].cpu().numpy().astype(np.int64), want)
+    assert np.array_equal(keys_s.cpu().numpy(), k[want])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fname", ["small_pe.bam", "edge_unsorted_l1.bam", "edge_uniform_long.bam"])
+def test_single_gpu_decode_sort_matches_oracle(gpu_ctx, oracle_mod, fname):
+    import torch
+    from hadoop_bam import sort
+    data = np.fromfile(os.path.join(GOLDEN, fname), dtype=np.uint8)
+    want_k, want_v, want_p, want_off, cols = _oracle_sorted(data)
+    d = torch.from_numpy(data).cuda()
+    h = gpu_ctx.parse_header(d)
+    rc, dc = gpu_ctx.decode_split_device(d, h["first_voffset"], (len(data) << 16) | 0xffff,
+                                         h["n_ref"])
+    assert rc == 0 and dc.status == 0 and dc.n_records == cols["n"]
+    run = sort.HipSortOps(gpu_ctx).run_from_columns(dc)
+    assert np.array_equal(run.keys.cpu().numpy(), want_k)
+    assert np.array_equal(run.voffset.cpu().numpy(), want_v)
+    assert np.array_equal(run.offsets.cpu().numpy(), want_off)
+    assert run.payload.cpu().numpy().tobytes() == want_p.tobytes()
+
+
+@pytest.mark.gpu
+def test_sort_received_chunks_equals_global_order(gpu_ctx, oracle_mod):
+    """The receive side of the exchange on the device: two source chunks (file order), each
+    locally sorted, re-sorted stably == the oracle's total order."""
+    import torch
+    from hadoop_bam import sort
+    data = np.fromfile(os.path.join(GOLDEN, "edge_unsorted_l1.bam"), dtype=np.uint8)
+    want_k, want_v, want_p, _, cols = _oracle_sorted(data)
+    pay, off = oracle_mod.record_payloads(cols)
+    n = cols["n"]
+    cut = n // 2
+    parts = []
+    for lo, hi in ((0, cut), (cut, n)):
+        o = lo + oracle_mod.sort_order(cols["key"][lo:hi])
+        no, npay = oracle_mod._regather(pay, off, o)
+        parts.append((cols["key"][o], cols["voffset"].astype(np.int64)[o], cols["block_size"][o], npay))
+    cat = lambda i, dt: torch.from_numpy(np.concatenate([p[i] for p in parts]).astype(dt)).cuda()
+    out = sort.HipSortOps(gpu_ctx).sort_received(cat(0, np.int64), cat(1, np.int64),
+                                                 cat(2, np.int32), cat(3, np.uint8))
+    assert np.array_equal(out.keys.cpu().numpy(), want_k)
+    assert np.array_equal(out.voffset.cpu().numpy(), want_v)
+    assert out.payload.cpu().numpy().tobytes() == want_p.tobytes()
