@@ -157,7 +157,8 @@ __global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __
                                                                uint32_t* __restrict__ tails,
                                                                int32_t* __restrict__ status,
                                                                int retry_only) {
-  __shared__ uint16_t s_ll[INFLATE_WG * 288];
+  // 320 B of LDS per lane (u8 lit/len symbols): 20 KiB per workgroup -> 8 per CU
+  __shared__ uint8_t s_ll[INFLATE_WG * 288];
   __shared__ uint8_t s_d[INFLATE_WG * 32];
   const uint32_t b = blockIdx.x * INFLATE_WG + threadIdx.x;
   if (b >= nblk) return;

@@ -92,6 +92,9 @@ struct Huff {
                      // doff[0] = off[0], doff[k] = off[k] - off[k-1] (an add chain keeps the
                      // compiler from rewriting the select chain into a scratch-indexed load)
   uint32_t empty;    // no codes at all (zlib max == 0)
+  uint32_t hlim[15]; // lit/len only: left-justified start of the length-l codes whose symbols
+                     // are >= 256 (canonical order puts them last within a length), so a u8
+                     // symbol table plus one compare recovers the 9-bit symbol
 };
 
 // code length / symbol index for a left-justified 15-bit value; returns false if invalid
@@ -108,6 +111,24 @@ __device__ __forceinline__ bool huff_lookup(const Huff& h, uint32_t v, uint32_t&
   idx = o + (int32_t)(v >> (15u - l));
   return v < h.lim[14];
 }
+// huff_lookup plus the symbol's bit 8 (lit/len tables built with kind 1)
+__device__ __forceinline__ bool huff_lookup_hi(const Huff& h, uint32_t v, uint32_t& L, int32_t& idx,
+                                               uint32_t& hi) {
+  uint32_t l = 1;
+  int32_t o = h.doff[0];
+  uint32_t t = h.hlim[0];
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const bool ge = v >= h.lim[k];
+    l += ge ? 1u : 0u;
+    o += ge ? h.doff[k + 1] : 0;
+    t = ge ? h.hlim[k + 1] : t;
+  }
+  L = l;
+  idx = o + (int32_t)(v >> (15u - l));
+  hi = v >= t ? 256u : 0u;
+  return v < h.lim[14];
+}
 
 // Build canonical tables from code lengths lens[0..n) (global scratch).  kind: 0 = code
 // lengths (CODES), 1 = lit/len (LENS), 2 = distances (DISTS).  Returns false on zlib's
@@ -115,13 +136,17 @@ __device__ __forceinline__ bool huff_lookup(const Huff& h, uint32_t v, uint32_t&
 template <typename SymT>
 __device__ __forceinline__ bool huff_build(const uint8_t* __restrict__ lens, int n, SymT* __restrict__ syms,
                            Huff& h, int kind) {
-  uint32_t cnt[16];
+  uint32_t cnt[16], nhi[16];
 #pragma unroll
-  for (int L = 0; L < 16; ++L) cnt[L] = 0;
+  for (int L = 0; L < 16; ++L) cnt[L] = nhi[L] = 0;
   for (int s = 0; s < n; ++s) {
     const uint32_t len = lens[s];
+    const uint32_t h = (kind == 1 && s >= 256) ? 1u : 0u;
 #pragma unroll
-    for (int L = 1; L < 16; ++L) cnt[L] += (len == (uint32_t)L) ? 1u : 0u;
+    for (int L = 1; L < 16; ++L) {
+      cnt[L] += (len == (uint32_t)L) ? 1u : 0u;
+      nhi[L] += (len == (uint32_t)L) ? h : 0u;
+    }
   }
   uint32_t maxl = 0;
 #pragma unroll
@@ -144,6 +169,7 @@ __device__ __forceinline__ bool huff_build(const uint8_t* __restrict__ lens, int
 #pragma unroll
   for (int L = 1; L < 16; ++L) {
     h.lim[L - 1] = (code + cnt[L]) << (15 - L);
+    h.hlim[L - 1] = (code + cnt[L] - nhi[L]) << (15 - L);
     const int32_t off = (int32_t)base - (int32_t)code;
     h.doff[L - 1] = off - prev_off;
     prev_off = off;
@@ -153,7 +179,7 @@ __device__ __forceinline__ bool huff_build(const uint8_t* __restrict__ lens, int
   }
   if (maxl == 0) {
 #pragma unroll
-    for (int L = 0; L < 15; ++L) h.lim[L] = 0;
+    for (int L = 0; L < 15; ++L) h.lim[L] = h.hlim[L] = 0;
   }
   for (int s = 0; s < n; ++s) {
     const uint32_t len = lens[s];
@@ -289,11 +315,12 @@ struct TokenSink {
 };
 
 // Inflate one raw DEFLATE stream (cdata, nbytes) to exactly isize bytes through `sink`.
-// syms_ll: 288 u16 LDS slots; syms_d: 32 u8 LDS slots; lens: 352 B global scratch.
-// Returns INF_OK / INF_SHORT / INF_DATA; *produced = bytes accounted.
-template <typename Sink>
+// syms_ll: 288 LDS slots, u16 (symbol) or u8 (symbol & 255; bit 8 from Huff.hlim, which halves
+// the batched inflate's LDS so two waves fit per SIMD); syms_d: 32 u8 LDS slots; lens: 352 B
+// global scratch.  Returns INF_OK / INF_SHORT / INF_DATA; *produced = bytes accounted.
+template <typename Sink, typename LLT>
 __device__ int32_t inflate_core(const uint8_t* __restrict__ cdata, uint32_t nbytes, uint32_t isize,
-                                uint16_t* __restrict__ syms_ll, uint8_t* __restrict__ syms_d,
+                                LLT* __restrict__ syms_ll, uint8_t* __restrict__ syms_d,
                                 uint8_t* __restrict__ lens, Sink& sink, uint32_t* produced) {
   BitIn br;
   br_init(br, cdata, nbytes);
@@ -331,7 +358,7 @@ __device__ int32_t inflate_core(const uint8_t* __restrict__ cdata, uint32_t nbyt
       for (int s = 0; s < 288; ++s)
         lens[s] = (uint8_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
       for (int s = 0; s < 32; ++s) lens[288 + s] = 5;
-      huff_build<uint16_t>(lens, 288, syms_ll, hl, 1);
+      huff_build<LLT>(lens, 288, syms_ll, hl, 1);
       huff_build<uint8_t>(lens + 288, 32, syms_d, hd, 2);
     } else if (type == 2u) {
       br_refill(br);
@@ -353,7 +380,7 @@ __device__ int32_t inflate_core(const uint8_t* __restrict__ cdata, uint32_t nbyt
         br_drop(br, 3);
       }
       Huff hc;
-      if (!huff_build<uint16_t>(lens, 19, syms_ll, hc, 0)) { rc = INF_DATA; goto done; }
+      if (!huff_build<LLT>(lens, 19, syms_ll, hc, 0)) { rc = INF_DATA; goto done; }
       // literal/length + distance code lengths (stored after the 19 CL lengths)
       uint8_t* ll = lens + 19;
       const uint32_t total = nlen + ndist;
@@ -396,7 +423,7 @@ __device__ int32_t inflate_core(const uint8_t* __restrict__ cdata, uint32_t nbyt
         for (uint32_t k = 0; k < rep; ++k) ll[have++] = v8;
       }
       if (ll[256] == 0) { rc = INF_DATA; goto done; }
-      if (!huff_build<uint16_t>(ll, (int)nlen, syms_ll, hl, 1)) { rc = INF_DATA; goto done; }
+      if (!huff_build<LLT>(ll, (int)nlen, syms_ll, hl, 1)) { rc = INF_DATA; goto done; }
       if (!huff_build<uint8_t>(ll + nlen, (int)ndist, syms_d, hd, 2)) { rc = INF_DATA; goto done; }
     } else {
       rc = INF_DATA;  // invalid block type
@@ -408,13 +435,14 @@ __device__ int32_t inflate_core(const uint8_t* __restrict__ cdata, uint32_t nbyt
       uint32_t L;
       int32_t idx;
       const uint32_t v = br_rev15(br);
-      const bool ok = huff_lookup(hl, v, L, idx);
+      uint32_t hi = 0;
+      const bool ok = sizeof(LLT) == 1 ? huff_lookup_hi(hl, v, L, idx, hi) : huff_lookup(hl, v, L, idx);
       if (!ok) {
         if (br_avail(br) >= 1u) { rc = INF_DATA; goto done; }
         goto leave;
       }
       if (L > br_avail(br)) goto leave;
-      const uint32_t sym = syms_ll[idx];
+      const uint32_t sym = (uint32_t)syms_ll[idx] | hi;
       br_drop(br, L);
       if (sym < 256u) {
         if (op == isize) goto leave;
