@@ -1398,6 +1398,29 @@ extern "C" int hbam_permute(hbam_ctx* c, const void* src, uint32_t elem_size, co
   return HBAM_OK;
 }
 
+extern "C" int64_t hbam_splitting_index(hbam_ctx* c, const hbam_columns* dv, int32_t granularity,
+                                       uint64_t file_len, uint64_t* out, uint64_t cap) {
+  if (!c || !dv || !out || granularity <= 0) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t n = dv->n_records;
+  if (n == 0 && dv->status == HBAM_OK)
+    return set_err(c, HBAM_EINVAL, "hbam_splitting_index: the split holds no record (first voffset unknown)");
+  if (dv->status != HBAM_OK) return set_err(c, dv->status, "hbam_splitting_index: decode raised %d", dv->status);
+  const uint64_t k = n / (uint64_t)granularity;
+  const uint64_t total = k + 2;
+  if (total > cap) return set_err(c, HBAM_EINVAL, "hbam_splitting_index: %llu entries > cap %llu",
+                                  (unsigned long long)total, (unsigned long long)cap);
+  uint64_t* d;
+  int rc;
+  if ((rc = ensure(c, B_S_OFF, k + 1, &d))) return rc;
+  if (k) k_index_pick<<<grid_for(k, RS_WG), RS_WG, 0, c->stream>>>(dv->voffset, n, (uint32_t)granularity, d);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, copy_sync(c, out, dv->voffset, 8, hipMemcpyDeviceToHost));
+  HIPCHK(c, copy_sync(c, out + 1, d, 8 * k, hipMemcpyDeviceToHost));
+  out[k + 1] = file_len << 16;
+  return (int64_t)total;
+}
+
 #ifdef HBAM_PROF
 // Profiling build only: attach a device buffer of 16 u64 per block for the per-block cycle
 // counters of k_inflate_tokens / k_resolve (tools/profile_inflate.py --prof).

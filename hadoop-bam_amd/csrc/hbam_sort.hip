@@ -167,4 +167,13 @@ __global__ __launch_bounds__(RS_WG) void k_gather_records(const uint8_t* __restr
   }
 }
 
+// SplittingBAMIndexer (SplittingBAMIndexer.java:146-248): the voffset before every
+// granularity-th record (records counted from 1) of a whole-file decode
+__global__ __launch_bounds__(RS_WG) void k_index_pick(const uint64_t* __restrict__ voffset, uint64_t n,
+                                                      uint32_t g, uint64_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * RS_WG + threadIdx.x;  // output entry j: record (j+1)*g-1
+  const uint64_t r = (j + 1) * (uint64_t)g - 1;
+  if (r < n) out[j] = voffset[r];
+}
+
 }  // namespace hbam

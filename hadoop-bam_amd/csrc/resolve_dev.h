@@ -7,7 +7,7 @@
 //
 // The block is walked in stretches of RS_S output bytes.  LDS holds a window of the RS_W
 // bytes before the stretch, the stretch and the next stretch (matches spill up to 258 bytes
-// past their stretch), 12 KiB per wave in all, so ~11 blocks share a CU.  Per stretch:
+// past their stretch), ~12 KiB per wave in all (with the record list), so ~13 blocks share a CU.  Per stretch:
 //   1. the stretch's match starts come from 64 bitmap words (one per lane), their
 //      descriptors are read once into an LDS record list and split into
 //        - "pre" matches: source ends before the stretch — every source byte is final —
@@ -23,8 +23,11 @@
 
 namespace hbam {
 
+#ifndef HBAM_RS_W
+#define HBAM_RS_W 1024  // A/B at 2 GB: 4096 -> 20.0 ms, 2048 -> 18.0, 1024 -> 16.7 (LDS -> occupancy)
+#endif
 constexpr uint32_t RS_S = 2048;                       // stretch (output bytes)
-constexpr uint32_t RS_W = 4096;                       // window kept in LDS behind the stretch
+constexpr uint32_t RS_W = HBAM_RS_W;                  // window kept in LDS behind the stretch
 constexpr uint32_t RS_BUF = RS_W + 2 * RS_S + 48;     // + pad for 32-byte over-reads
 constexpr uint32_t RS_MAXM = RS_S / 3 + 2;            // matches starting in one stretch
 

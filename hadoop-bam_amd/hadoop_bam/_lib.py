@@ -44,7 +44,7 @@ EXPORTS = [
     "hbam_decode_split", "hbam_columns_to_host", "hbam_free_host_columns",
     "hbam_release_columns", "hbam_guess_bam_record_start", "hbam_guess_batch",
     "hbam_guess_bgzf_block_start", "hbam_probabilistic_splits",
-    "hbam_sort_keys", "hbam_gather_records", "hbam_permute",
+    "hbam_sort_keys", "hbam_gather_records", "hbam_permute", "hbam_splitting_index",
 ]
 
 
@@ -147,6 +147,8 @@ def load(path=None):
         "hbam_gather_records": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, vp, C.c_uint64, vp,
                                           C.POINTER(C.c_uint64)]),
         "hbam_permute": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint64, vp]),
+        "hbam_splitting_index": (C.c_int64, [vp, C.POINTER(Columns), C.c_int32, C.c_uint64, vp,
+                                             C.c_uint64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -336,3 +338,21 @@ class Context:
         if r < 0:
             return r, None, None
         return r, vs[:r], ve[:r]
+
+    def splitting_index(self, data, granularity=4096):
+        """SplittingBAMIndexer over a whole BAM file on the device -> uint64 entries."""
+        p, n, dev, keep = self._ptr(data)
+        h = self.parse_header(data)
+        if not isinstance(h, dict):
+            return h, None
+        d = Columns()
+        rc = self.L.hbam_decode_split(self.h, p, dev, 0, n, n, h["first_voffset"],
+                                      (n << 16) | 0xffff, h["n_ref"], C.byref(d))
+        if rc:
+            return rc, None
+        cap = int(d.n_records) // granularity + 2
+        out = np.zeros(cap, np.uint64)
+        r = self.L.hbam_splitting_index(self.h, C.byref(d), granularity, n, out.ctypes.data, cap)
+        if r < 0:
+            return int(r), None
+        return 0, out[:r]

@@ -242,6 +242,28 @@ class BGZFSplitGuesser:
         return int(r)
 
 
+class SplittingBAMIndexer:
+    """SplittingBAMIndexer.java:146-248 on the device: index(bam_bytes, out) writes the
+    big-endian u64 entries (first record voffset, every granularity-th record's voffset,
+    file_len<<16) that SplittingBAMIndex reads."""
+
+    DEFAULT_GRANULARITY = 4096
+
+    def __init__(self, granularity=DEFAULT_GRANULARITY, ctx=None):
+        self.granularity = int(granularity)
+        self.ctx = ctx
+
+    def index(self, data, out=None):
+        from ._lib import Context
+        ctx = self.ctx or Context(0)
+        rc, offs = ctx.splitting_index(data, self.granularity)
+        raise_for(rc, ctx.last_error())
+        raw = b"".join(struct.pack(">q", int(x)) for x in offs)
+        if out is not None:
+            out.write(raw)
+        return raw
+
+
 class SplittingBAMIndex:
     """SplittingBAMIndex.java:50-77 — big-endian u64 voffsets + file_len<<16."""
 

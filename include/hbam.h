@@ -208,6 +208,13 @@ int hbam_sort_keys(hbam_ctx* ctx, const int64_t* keys, uint64_t n, int64_t* keys
 int hbam_gather_records(hbam_ctx* ctx, const uint8_t* ubuf, const uint64_t* rec_off,
                         const int32_t* block_size, const uint32_t* perm, uint64_t n, uint8_t* out,
                         uint64_t out_cap, uint64_t* out_off, uint64_t* total_bytes);
+/* SplittingBAMIndexer (SplittingBAMIndexer.java:146-248, §8 f-2) from a whole-file decode
+ * (dv: device columns of hbam_decode_split over [first record, len<<16|0xffff]): out (host)
+ * = voffset of the first record, the voffset before every granularity-th record, then
+ * file_len<<16 — the entries SplittingBAMIndex.java:50-77 reads (big-endian on disk).
+ * Returns the entry count or a negative code. */
+int64_t hbam_splitting_index(hbam_ctx* ctx, const hbam_columns* dv, int32_t granularity,
+                             uint64_t file_len, uint64_t* out, uint64_t cap);
 /* out[i] = src[perm[i]] for elem_size 4 or 8 (device pointers): carries a column (voffset,
  * block_size) through a sort permutation. */
 int hbam_permute(hbam_ctx* ctx, const void* src, uint32_t elem_size, const uint32_t* perm,

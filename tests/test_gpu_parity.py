@@ -269,3 +269,14 @@ def test_parallel_inflate_retry_path_on_corruption(oracle_mod):
         assert int(st[i]) == codes[orc], (i, int(st[i]), orc)
         if orc == 0:
             assert u[int(off[i]):int(off[i + 1])].tobytes() == out
+
+
+# ---- SplittingBAMIndexer on the device ----------------------------------
+@pytest.mark.parametrize("fname", ["small_pe.bam", "edge_uniform_long.bam", "edge_unsorted_l1.bam"])
+@pytest.mark.parametrize("g", [1, 7, 1024, 4096])
+def test_splitting_index_matches_oracle(gpu_ctx, oracle_mod, fname, g):
+    data = _load(fname)
+    want = oracle_mod.splitting_index(data, granularity=g)
+    rc, got = gpu_ctx.splitting_index(data, g)
+    assert rc == 0, gpu_ctx.last_error()
+    assert np.array_equal(got, want)
