@@ -288,18 +288,19 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     const uint64_t g = abase + (uint64_t)k * RS_S + 16u * lane;
     if (k < nstr) {
       r0 = *(const uint4*)(ubuf + g);
-      r1 = *(const uint4*)(ubuf + g + 1024);
+      if (RS_C == 2) r1 = *(const uint4*)(ubuf + g + 1024);
     }
   };
   uint4 ra0 = make_uint4(0, 0, 0, 0), ra1 = ra0, rb0 = ra0, rb1 = ra0;
   load_raw(0, ra0, ra1);
   load_raw(1, rb0, rb1);
   *(uint4*)(s_buf + RS_W + 16u * lane) = ra0;
-  *(uint4*)(s_buf + RS_W + 1024 + 16u * lane) = ra1;
+  if (RS_C == 2) *(uint4*)(s_buf + RS_W + 1024 + 16u * lane) = ra1;
   *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = rb0;
-  *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = rb1;
+  if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = rb1;
   load_raw(2, ra0, ra1);  // ra = raw[k+2] during stretch k
-  uint32_t wnext = (lane < nwords) ? bm[lane] : 0u;
+  constexpr uint32_t WPS = RS_S / 32;  // bitmap words per stretch (<= 64: one per lane)
+  uint32_t wnext = (lane < WPS && lane < nwords) ? bm[lane] : 0u;
   __syncthreads();
 #ifdef HBAM_PROF
   p_st = PROF_CLK() - pc0;
@@ -308,8 +309,8 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     const uint32_t s0 = k * RS_S;
     const uint32_t word = wnext;
     {
-      const uint32_t wi = (k + 1) * (RS_S / 32) + lane;
-      wnext = (k + 1 < nstr && wi < nwords) ? bm[wi] : 0u;
+      const uint32_t wi = (k + 1) * WPS + lane;
+      wnext = (lane < WPS && k + 1 < nstr && wi < nwords) ? bm[wi] : 0u;
     }
     // LDS index of block offset x: x - s0 + RS_W + a0
     const uint32_t lbase = RS_W + a0 - s0;
@@ -420,7 +421,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     for (uint32_t i = 0; i < (RS_W + RS_S) / 1024; ++i)
       *(uint4*)(s_buf + 1024u * i + 16u * lane) = *(const uint4*)(s_buf + RS_S + 1024u * i + 16u * lane);
     *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = ra0;
-    *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = ra1;
+    if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = ra1;
     load_raw(k + 3, ra0, ra1);
     __syncthreads();
   }

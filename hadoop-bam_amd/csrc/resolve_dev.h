@@ -24,9 +24,13 @@
 namespace hbam {
 
 #ifndef HBAM_RS_W
-#define HBAM_RS_W 1024  // A/B at 2 GB: 4096 -> 20.0 ms, 2048 -> 18.0, 1024 -> 16.7 (LDS -> occupancy)
+#define HBAM_RS_W 1024  // A/B at 2 GB (stretch 2 KiB): 4096 -> 20.0 ms, 2048 -> 18.0, 1024 -> 16.7; 0 is not supported
 #endif
-constexpr uint32_t RS_S = 2048;                       // stretch (output bytes)
+#ifndef HBAM_RS_S
+#define HBAM_RS_S 1024  // A/B at 2 GB (window 1 KiB): 2048 -> 16.8 ms, 1024 -> 11.7 ms
+#endif
+constexpr uint32_t RS_S = HBAM_RS_S;                  // stretch (output bytes): 1024 or 2048
+constexpr uint32_t RS_C = RS_S / 1024;                // 16-byte columns per lane per stretch
 constexpr uint32_t RS_W = HBAM_RS_W;                  // window kept in LDS behind the stretch
 constexpr uint32_t RS_BUF = RS_W + 2 * RS_S + 48;     // + pad for 32-byte over-reads
 constexpr uint32_t RS_MAXM = RS_S / 3 + 2;            // matches starting in one stretch
