@@ -942,6 +942,70 @@ out:
   return n;
 }
 
+/* FileInputStream.read into dst: up to k bytes, 0 at or past EOF. */
+static int bi_read(const uint8_t* f, uint64_t len, uint64_t* at, uint8_t* dst, int k) {
+  if (*at >= len) return 0;
+  const uint64_t avail = len - *at;
+  const int got = avail < (uint64_t)k ? (int)avail : k;
+  memcpy(dst, f + *at, (size_t)got);
+  *at += (uint64_t)got;
+  return got;
+}
+
+/* BGZFBlockIndexer.index + skipBlock (util/BGZFBlockIndexer.java:97-181) over a plain
+ * FileInputStream: reads at or past EOF return 0 bytes; InputStream.skip on a file moves the
+ * position by the full request even past EOF (so a truncated final block still counts).
+ * Reference quirk kept: `pos` is a Java int (:88), so past 2 GiB it wraps and the entry is
+ * the low 48 bits of the sign-extended value (lb.put(0, pos), :115-116).  Entries: `pos`
+ * after every granularity-th block, then file.length() (:124-125).  Returns the count or
+ * OR_EIO (the IOException ioError/"block without BGZF subfield" raise). */
+int64_t or_bgzf_block_index(const uint8_t* f, uint64_t len, int32_t granularity, uint64_t* out,
+                            uint64_t cap) {
+  if (granularity <= 0) return OR_EIO;
+  uint64_t at = 0;  /* FileInputStream position */
+  int32_t pos = 0;  /* the indexer's int `pos` */
+  int64_t n = 0;
+  for (int32_t i = 0;;) {
+    uint8_t bb[8];
+    int got = bi_read(f, len, &at, bb, 4);
+    if (got != 4) {
+      if (got == 0) break;
+      return OR_EIO; /* "too short, no ID/CM/FLG" */
+    }
+    if (((uint32_t)bb[0] << 24 | (uint32_t)bb[1] << 16 | (uint32_t)bb[2] << 8 | bb[3]) != 0x1f8b0804u)
+      return OR_EIO;
+    if (bi_read(f, len, &at, bb, 8) != 8) return OR_EIO; /* "no XLEN" */
+    const int xlen = bb[6] | bb[7] << 8;
+    int found = 0;
+    for (int off = 0; off < xlen;) {
+      if (bi_read(f, len, &at, bb, 4) != 4) return OR_EIO;
+      off += 4;
+      const uint32_t si = (uint32_t)bb[0] << 24 | (uint32_t)bb[1] << 16 | (uint32_t)bb[2] << 8 | bb[3];
+      if ((si & ~0xffu) == 0x42430200u) {
+        if (bi_read(f, len, &at, bb, 2) != 2) return OR_EIO; /* "missing BSIZE" */
+        off += 2;
+        const int bsize = bb[0] | bb[1] << 8;
+        const int64_t skip = (int64_t)(xlen - off) + (bsize - xlen - 19) + 8;
+        if (skip > 0) at += (uint64_t)skip; /* fullySkip: for (s = skip; s > 0;) */
+        pos = (int32_t)((uint32_t)pos + (uint32_t)(bsize + 1));
+        found = 1;
+        break;
+      }
+      const int slen = bb[2] | bb[3] << 8;
+      if (slen > 0) at += (uint64_t)slen;
+      off += slen;
+    }
+    if (!found) return OR_EIO; /* "block without BGZF subfield" */
+    if (++i == granularity) {
+      i = 0;
+      if ((uint64_t)n < cap) out[n] = (uint64_t)(int64_t)pos & 0xffffffffffffull;
+      ++n;
+    }
+  }
+  if ((uint64_t)n < cap) out[n] = len & 0xffffffffffffull;
+  return n + 1;
+}
+
 /* ------------------------------------------------------------------------------ */
 /* Columnar capture of the split reader (test/baseline helper).                      */
 typedef struct cols_ctx {

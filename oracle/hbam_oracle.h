@@ -114,6 +114,11 @@ int64_t or_probabilistic_splits(const uint8_t* f, uint64_t len, const uint64_t* 
 int64_t or_splitting_index(const uint8_t* f, uint64_t len, int32_t granularity, uint64_t* out,
                            uint64_t cap);
 
+/* BGZFBlockIndexer.index (util/BGZFBlockIndexer.java:97-181): compressed offset after every
+ * granularity-th BGZF block (int `pos`, wraps past 2 GiB), then the file length.  Returns
+ * the entry count or OR_EIO. */
+int64_t or_bgzf_block_index(const uint8_t* f, uint64_t len, int32_t granularity, uint64_t* out,
+                            uint64_t cap);
 
 /* Columnar capture of or_read_split (for parity tests and the CPU baseline). */
 typedef struct or_cols {

@@ -54,6 +54,8 @@ def lib():
                                               C.c_void_p, C.c_void_p]
         L.or_splitting_index.restype = C.c_int64
         L.or_splitting_index.argtypes = [u8p, C.c_uint64, C.c_int32, C.c_void_p, C.c_uint64]
+        L.or_bgzf_block_index.restype = C.c_int64
+        L.or_bgzf_block_index.argtypes = [u8p, C.c_uint64, C.c_int32, C.c_void_p, C.c_uint64]
         L.or_read_split_cols.restype = C.c_int
         L.or_read_split_cols.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_int,
                                          C.POINTER(OrCols)]
@@ -195,6 +197,18 @@ def splitting_index(data, granularity=4096):
     cap = 1 << 20
     out = np.zeros(cap, np.uint64)
     n = lib().or_splitting_index(p, len(a), granularity, out.ctypes.data, cap)
+    if n < 0:
+        return n
+    return out[:n]
+
+
+def bgzf_block_index(data, granularity=1):
+    """BGZFBlockIndexer.index (util/BGZFBlockIndexer.java:97-181): u64 entries (48-bit
+    values) or a negative code."""
+    a, p = _buf(data)
+    cap = len(a) // 28 + 2
+    out = np.zeros(cap, np.uint64)
+    n = lib().or_bgzf_block_index(p, len(a), granularity, out.ctypes.data, cap)
     if n < 0:
         return n
     return out[:n]
