@@ -1421,6 +1421,39 @@ extern "C" int64_t hbam_splitting_index(hbam_ctx* c, const hbam_columns* dv, int
   return (int64_t)total;
 }
 
+extern "C" int64_t hbam_bgzf_block_index(hbam_ctx* c, const uint8_t* file, int on_device,
+                                        uint64_t len, int32_t granularity, uint64_t* out,
+                                        uint64_t cap) {
+  if (!c || (!file && len) || !out || granularity <= 0) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (len == 0) {  // no block: only the terminating file length (:124-125)
+    if (cap < 1) return set_err(c, HBAM_EINVAL, "hbam_bgzf_block_index: cap 0");
+    out[0] = 0;
+    return 1;
+  }
+  const uint8_t* d;
+  int rc = stage_comp(c, file, on_device, len, &d);
+  if (rc) return rc;
+  Chain ch;
+  if ((rc = build_chain(c, d, len, 0, true, &ch))) return rc;
+  if (ch.end_code != HBAM_EEOF)  // skipBlock's ioError (:133-180)
+    return set_err(c, HBAM_EIO, "hbam_bgzf_block_index: no BGZF block at %llu",
+                   (unsigned long long)ch.end_pos);
+  const uint64_t k = ch.nb / (uint64_t)granularity;
+  if (k + 1 > cap) return set_err(c, HBAM_EINVAL, "hbam_bgzf_block_index: %llu entries > cap %llu",
+                                  (unsigned long long)(k + 1), (unsigned long long)cap);
+  if (k) {
+    uint64_t* dout;
+    if ((rc = ensure(c, B_S_OFF, k, &dout))) return rc;
+    k_bgzfi_pick<<<grid_for(k, RS_WG), RS_WG, 0, c->stream>>>((const BlockRec*)c->bufs[B_BLK].p, ch.nb,
+                                                              len, (uint32_t)granularity, k, dout);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, copy_sync(c, out, dout, 8 * k, hipMemcpyDeviceToHost));
+  }
+  out[k] = len & 0xffffffffffffull;
+  return (int64_t)(k + 1);
+}
+
 #ifdef HBAM_PROF
 // Profiling build only: attach a device buffer of 16 u64 per block for the per-block cycle
 // counters of k_inflate_tokens / k_resolve (tools/profile_inflate.py --prof).

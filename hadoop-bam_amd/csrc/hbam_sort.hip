@@ -176,4 +176,17 @@ __global__ __launch_bounds__(RS_WG) void k_index_pick(const uint64_t* __restrict
   if (r < n) out[j] = voffset[r];
 }
 
+// BGZFBlockIndexer.index (util/BGZFBlockIndexer.java:109-122): entry j = the indexer's int
+// `pos` after block (j+1)*g, i.e. the next block's offset (or the file length after the last
+// block), as the low 48 bits of the sign-extended Java int (wraps past 2 GiB, :88,115-116).
+__global__ __launch_bounds__(RS_WG) void k_bgzfi_pick(const BlockRec* __restrict__ blk, uint64_t nb,
+                                                      uint64_t file_len, uint32_t g,
+                                                      uint64_t k, uint64_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * RS_WG + threadIdx.x;
+  if (j >= k) return;
+  const uint64_t b = (j + 1) * (uint64_t)g;
+  const uint64_t p = b < nb ? blk[b].coff : file_len;
+  out[j] = (uint64_t)(int64_t)(int32_t)(uint32_t)p & 0xffffffffffffull;
+}
+
 }  // namespace hbam

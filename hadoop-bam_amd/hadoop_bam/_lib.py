@@ -149,6 +149,8 @@ def load(path=None):
         "hbam_permute": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint64, vp]),
         "hbam_splitting_index": (C.c_int64, [vp, C.POINTER(Columns), C.c_int32, C.c_uint64, vp,
                                              C.c_uint64]),
+        "hbam_bgzf_block_index": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_int32, vp,
+                                              C.c_uint64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -353,6 +355,17 @@ class Context:
         cap = int(d.n_records) // granularity + 2
         out = np.zeros(cap, np.uint64)
         r = self.L.hbam_splitting_index(self.h, C.byref(d), granularity, n, out.ctypes.data, cap)
+        if r < 0:
+            return int(r), None
+        return 0, out[:r]
+
+    def bgzf_block_index(self, data, granularity=1):
+        """BGZFBlockIndexer.index (util/BGZFBlockIndexer.java:97-181) on the device ->
+        (rc, uint64 entries)."""
+        p, n, dev, keep = self._ptr(data)
+        cap = n // 28 // max(int(granularity), 1) + 2  # a BGZF block is at least 28 bytes
+        out = np.zeros(cap, np.uint64)
+        r = self.L.hbam_bgzf_block_index(self.h, p, dev, n, int(granularity), out.ctypes.data, cap)
         if r < 0:
             return int(r), None
         return 0, out[:r]

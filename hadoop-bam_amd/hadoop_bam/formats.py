@@ -300,6 +300,134 @@ class SplittingBAMIndex:
         return len(self.offsets)
 
 
+class BGZFBlockIndexer:
+    """util/BGZFBlockIndexer.java:41-225 on the device: index(bgzf_bytes, out) writes, for
+    every granularity-th block, the offset after it as a big-endian 48-bit integer, then the
+    file length ([file].bgzfi).  Like the reference, offsets past 2 GiB wrap (int `pos`)."""
+
+    def __init__(self, granularity, ctx=None):
+        if int(granularity) <= 0:
+            raise IllegalArgumentException(
+                "Granularity must be a positive integer, not '%s'!" % granularity)
+        self.granularity = int(granularity)
+        self.ctx = ctx
+
+    def index(self, data, out=None):
+        ctx = self.ctx or context()
+        if isinstance(data, str):
+            path, data = data, _read_file(data)
+        else:
+            path = None
+        rc, offs = ctx.bgzf_block_index(data, self.granularity)
+        raise_for(rc, ctx.last_error())
+        raw = b"".join(struct.pack(">q", int(x))[2:] for x in offs)
+        if out is None and path is not None:
+            with open(path + ".bgzfi", "wb") as f:
+                f.write(raw)
+        elif out is not None:
+            out.write(raw)
+        return raw
+
+
+class BGZFBlockIndex:
+    """util/BGZFBlockIndex.java:39-78 — 48-bit big-endian block offsets + the file size."""
+
+    def __init__(self, inp=None):
+        self.offsets = []
+        if inp is not None:
+            self.readIndex(inp)
+
+    def readIndex(self, inp):  # :50-69
+        data = inp.read() if hasattr(inp, "read") else _read_file(inp)
+        prev = -1
+        offs = set()
+        for i in range(0, len(data) - 5, 6):
+            cur = int.from_bytes(data[i:i + 6], "big")
+            if prev > cur:
+                raise IOException("Invalid BGZF block index; offsets not in order: %#x > %#x"
+                                  % (prev, cur))
+            offs.add(cur)
+            prev = cur
+        if len(offs) < 1:
+            raise IOException("Invalid BGZF block index: should contain at least the file size")
+        offs.add(0)
+        self.offsets = sorted(offs)
+
+    def prevBlock(self, file_pos):  # TreeSet.floor
+        import bisect
+        k = bisect.bisect_right(self.offsets, file_pos)
+        return self.offsets[k - 1] if k else None
+
+    def nextBlock(self, file_pos):  # TreeSet.higher
+        import bisect
+        k = bisect.bisect_right(self.offsets, file_pos)
+        return self.offsets[k] if k < len(self.offsets) else None
+
+    def size(self):
+        return len(self.offsets)
+
+    def fileSize(self):
+        return self.offsets[-1]
+
+
+class BGZFSplitFileInputFormat:
+    """util/BGZFSplitFileInputFormat.java:50-170: Hadoop FileSplits aligned to BGZF block
+    starts, from [path].bgzfi when present, else by BGZFSplitGuesser (device)."""
+
+    @staticmethod
+    def getIdxPath(path):
+        return str(path) + ".bgzfi"
+
+    def getSplits(self, splits, cfg=None):  # :51-81
+        cfg = cfg or Configuration()
+        splits = sorted(splits, key=lambda s: str(s.getPath()))
+        out, i = [], 0
+        while i < len(splits):
+            try:
+                i = self._add_indexed_splits(splits, i, out, cfg)
+            except IOException:
+                i = self._add_probabilistic_splits(splits, i, out, cfg)
+        return out
+
+    def _add_indexed_splits(self, splits, i, out, cfg):  # :85-122
+        path = splits[i].getPath()
+        try:
+            with open(self.getIdxPath(path), "rb") as f:
+                idx = BGZFBlockIndex(f)
+        except OSError as e:
+            raise IOException(str(e))
+        j_end = i
+        while j_end < len(splits) and splits[j_end].getPath() == path:
+            j_end += 1
+        for j in range(i, j_end):
+            fs = splits[j]
+            start, end = fs.getStart(), fs.getStart() + fs.getLength()
+            bs = idx.prevBlock(start)
+            be = idx.prevBlock(end) if j == j_end - 1 else idx.nextBlock(end)
+            if bs is None:
+                raise JavaRuntimeException("Internal error or invalid index: no block start for %d" % start)
+            if be is None:
+                raise JavaRuntimeException("Internal error or invalid index: no block end for %d" % end)
+            out.append(FileSplit(path, bs, be - bs, fs.getLocations()))
+        return j_end
+
+    def _add_probabilistic_splits(self, splits, i, out, cfg):  # :126-153
+        path = splits[i].getPath()
+        guesser = BGZFSplitGuesser(path, cfg)
+        while True:  # do { ... } while (i < size && fspl.getPath().equals(path))
+            fs = splits[i]
+            beg, end = fs.getStart(), fs.getStart() + fs.getLength()
+            aligned = guesser.guessNextBGZFBlockStart(beg, end)
+            out.append(FileSplit(path, aligned, end - aligned, fs.getLocations()))
+            i += 1
+            if not (i < len(splits) and fs.getPath() == path):
+                break
+        return i
+
+    def isSplitable(self, job=None, path=None):
+        return True
+
+
 # ---- record value -------------------------------------------------------------------
 class BAMRecordView:
     """A lazily decoded BAM record (the SAMRecord the reader hands out): fixed fields

@@ -215,6 +215,14 @@ int hbam_gather_records(hbam_ctx* ctx, const uint8_t* ubuf, const uint64_t* rec_
  * Returns the entry count or a negative code. */
 int64_t hbam_splitting_index(hbam_ctx* ctx, const hbam_columns* dv, int32_t granularity,
                              uint64_t file_len, uint64_t* out, uint64_t cap);
+/* BGZFBlockIndexer.index (util/BGZFBlockIndexer.java:97-181, §8 f-3): the whole BGZF file
+ * (host or device per on_device) -> out (host) = the compressed offset after every
+ * granularity-th block, then the file length: the 48-bit values written big-endian as
+ * [file].bgzfi and read by BGZFBlockIndex.java:50-69.  The indexer's `pos` is a Java int,
+ * so entries past 2 GiB are the low 48 bits of the sign-extended wrapped value, as there.
+ * Returns the entry count, HBAM_EIO where skipBlock raises IOException, or <0. */
+int64_t hbam_bgzf_block_index(hbam_ctx* ctx, const uint8_t* file, int on_device, uint64_t len,
+                              int32_t granularity, uint64_t* out, uint64_t cap);
 /* out[i] = src[perm[i]] for elem_size 4 or 8 (device pointers): carries a column (voffset,
  * block_size) through a sort permutation. */
 int hbam_permute(hbam_ctx* ctx, const void* src, uint32_t elem_size, const uint32_t* perm,
