@@ -45,6 +45,7 @@ EXPORTS = [
     "hbam_release_columns", "hbam_guess_bam_record_start", "hbam_guess_batch",
     "hbam_guess_bgzf_block_start", "hbam_probabilistic_splits",
     "hbam_sort_keys", "hbam_gather_records", "hbam_permute", "hbam_splitting_index",
+    "hbam_bgzf_block_index",
 ]
 
 
