@@ -224,7 +224,7 @@ def test_indexer_writes_reference_bytes(tmp_path, gpu_ctx, oracle_mod, small_bam
     got = BGZFSplitFileInputFormat().getSplits(splits)
     for s, o in zip(splits, got):
         st, en = s.getStart(), s.getStart() + s.getLength()
-        assert o.getStart() == oracle_mod.guess_bgzf_block_start(small_bam, st, en)
+        assert o.getStart() == oracle_mod.guess_bgzf_block_start(small_bam, st, en)[0]
         assert o.getStart() + o.getLength() == en
 
 
