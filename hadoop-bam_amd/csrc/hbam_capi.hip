@@ -1188,7 +1188,7 @@ extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device,
     HIPCHK(c, hipMemcpyAsync(w.end, end + g0, kb * 8, hipMemcpyHostToDevice, c->stream));
     GuessCache gc;
     if ((rc = build_guess_cache(c, d, file_len, w.beg, w.end, kb, &gc))) return rc;
-    k_guess_bam<<<grid_for(kb, GUESS_WG), GUESS_WG, 0, c->stream>>>(
+    k_guess_bam<<<grid_for(kb, GUESS_BAM_WG), GUESS_BAM_WG, 0, c->stream>>>(
         d, (int64_t)file_len, w.beg, w.end, (uint32_t)kb, n_ref, w.scratch, w.lens, w.bufs, w.out,
         w.err, gc.cn, gc.cbase, gc.cpos, gc.cblk, gc.cuoff, gc.cubuf, gc.cst, gc.ccrc);
     HIPCHK(c, hipGetLastError());

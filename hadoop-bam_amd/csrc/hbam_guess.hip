@@ -30,6 +30,13 @@ constexpr int32_t G_MAGIC = 0x04088b1f;
 constexpr int32_t G_MAGIC_SUB = 0x00024342;
 constexpr int32_t G_MAX_BYTES_READ = 3 * 0xffff + 0xfffe;
 constexpr uint32_t GUESS_WG = 64;
+#ifndef HBAM_GUESS_BAM_WG
+#define HBAM_GUESS_BAM_WG 64
+#endif
+// lanes (= guesses) per k_guess_bam workgroup.  A/B on config #3 (10k guesses, 2 GB file):
+// 64 -> 1.52 s, 8 -> 1.51 s, 4 -> 1.48 s: spreading guesses over more SIMDs does not help, the
+// batch time is set by its slowest guesses, so the default stays 64.
+constexpr uint32_t GUESS_BAM_WG = HBAM_GUESS_BAM_WG;
 constexpr uint32_t GC_CAP = 256;      // cached candidate blocks per guess window
 
 // Candidate blocks of one guess window (sorted absolute file offsets) and their inflated
@@ -488,7 +495,7 @@ __device__ void crc_table_init(uint32_t* T) {
 }
 
 // One lane per guess.  bufs[i] = initial 8-byte ByteBuffer state; written back at exit.
-__global__ __launch_bounds__(GUESS_WG) void k_guess_bam(const uint8_t* __restrict__ file, int64_t flen,
+__global__ __launch_bounds__(GUESS_BAM_WG) void k_guess_bam(const uint8_t* __restrict__ file, int64_t flen,
                                                         const int64_t* __restrict__ beg,
                                                         const int64_t* __restrict__ end, uint32_t k,
                                                         int32_t n_ref, uint8_t* __restrict__ scratch,
@@ -504,11 +511,11 @@ __global__ __launch_bounds__(GUESS_WG) void k_guess_bam(const uint8_t* __restric
                                                         const uint8_t* __restrict__ cubuf,
                                                         const int32_t* __restrict__ cst,
                                                         const uint32_t* __restrict__ ccrc) {
-  __shared__ uint16_t s_ll[GUESS_WG * 288];
-  __shared__ uint8_t s_d[GUESS_WG * 32];
+  __shared__ uint16_t s_ll[GUESS_BAM_WG * 288];
+  __shared__ uint8_t s_d[GUESS_BAM_WG * 32];
   __shared__ uint32_t T[256];
   crc_table_init(T);
-  const uint32_t i = blockIdx.x * GUESS_WG + threadIdx.x;
+  const uint32_t i = blockIdx.x * GUESS_BAM_WG + threadIdx.x;
   if (i >= k) return;
   Guesser g;
   g.n_ref = n_ref;
