@@ -173,6 +173,9 @@ int ensure(hbam_ctx* c, BufId id, size_t count, T** out) {
 }
 
 float ev_ms(hbam_ctx* c, int a, int b);
+#ifndef HBAM_GUESS_BATCH
+#define HBAM_GUESS_BATCH 16384  // guesses per launch (~64 KiB + cache each); config #3 A/B: 4096 -> 1.50 s, 16384 -> 0.094 s
+#endif
 inline uint32_t grid_for(uint64_t n, uint32_t wg) { return (uint32_t)((n + wg - 1) / wg); }
 
 // stream-ordered synchronous copy (the context stream is non-blocking: a plain hipMemcpy
@@ -1176,7 +1179,7 @@ extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device,
     }
   }
   HIPCHK(c, hipEventRecord(c->ev[9], c->stream));
-  const uint64_t batch = 4096;
+  const uint64_t batch = HBAM_GUESS_BATCH;
   for (uint64_t g0 = 0; g0 < k; g0 += batch) {
     const uint64_t kb = std::min(batch, k - g0);
     GuessWork w;
