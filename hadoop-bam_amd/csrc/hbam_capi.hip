@@ -123,7 +123,6 @@ struct hbam_ctx {
   hipEvent_t ev[16];
   hbam_timing timing{};
   uint64_t* pinned_small = nullptr;  // host pinned scalars
-  unsigned long long* retry_ctr = nullptr;  // device: blocks retried by the lane-per-block pass
 };
 
 namespace {
@@ -391,15 +390,8 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   if ((rc = ensure(c, B_BITMAP, nb * BITMAP_WORDS, &bitmap))) return rc;
   if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
   if (nb) {
-    if (c->opts.inflate_mode == 1) {  // wave-parallel Huffman pass + lane-per-block retry
-      k_inflate_par<<<(uint32_t)nb, PI_NL, 0, c->stream>>>(dcomp, blk, uoff, (uint32_t)nb, ubuf,
-                                                           bitmap, tails, st, c->retry_ctr);
-      k_inflate_tokens<<<grid_for(nb, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
-          dcomp, blk, uoff, (uint32_t)nb, ubuf, lens, bitmap, tails, st, 1);
-    } else {  // lane-per-block Huffman pass (default: faster on MI355X)
-      k_inflate_tokens<<<grid_for(nb, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
-          dcomp, blk, uoff, (uint32_t)nb, ubuf, lens, bitmap, tails, st, 0);
-    }
+    k_inflate_tokens<<<grid_for(nb, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
+        dcomp, blk, uoff, (uint32_t)nb, ubuf, lens, bitmap, tails, st);
     HIPCHK(c, hipEventRecord(c->ev[11], c->stream));
     k_resolve<<<(uint32_t)nb, 64, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, bitmap, tails, st);
   }
@@ -430,10 +422,6 @@ hbam_ctx* hbam_create(int device_ordinal, const hbam_opts* opts) {
     return nullptr;
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
-  if (hipMalloc((void**)&c->retry_ctr, 256) != hipSuccess || hipMemset(c->retry_ctr, 0, 256) != hipSuccess) {
-    delete c;
-    return nullptr;
-  }
   if (hipHostMalloc((void**)&c->pinned_small, 4096, hipHostMallocDefault) != hipSuccess) {
     delete c;
     return nullptr;
@@ -449,7 +437,6 @@ void hbam_destroy(hbam_ctx* c) {
     if (b.p) (void)hipFree(b.p);
   for (auto& e : c->ev) (void)hipEventDestroy(e);
   if (c->pinned_small) (void)hipHostFree(c->pinned_small);
-  if (c->retry_ctr) (void)hipFree(c->retry_ctr);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -460,14 +447,6 @@ int hbam_get_timing(const hbam_ctx* c, hbam_timing* out) {
   if (!c || !out) return HBAM_EINVAL;
   *out = c->timing;
   return HBAM_OK;
-}
-
-int hbam_inflate_stats(hbam_ctx* c, uint64_t* out, uint32_t n) {
-  if (!c || !out) return HBAM_EINVAL;
-  if (n > PI_NSTAT) n = PI_NSTAT;
-  HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, copy_sync(c, out, c->retry_ctr, 8ull * n, hipMemcpyDeviceToHost));
-  return (int)n;
 }
 
 int hbam_upload(hbam_ctx* c, const uint8_t* host, uint64_t len, uint8_t** dev_out) {
@@ -660,7 +639,6 @@ int hbam_inflate(hbam_ctx* c, const uint8_t* comp, int on_device, uint64_t comp_
   if ((rc = ensure(c, B_CRC, n + 1, &crc))) return rc;
   HIPCHK(c, hipMemcpyAsync(db, hb.data(), n * sizeof(BlockRec), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(duoff, uo.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->retry_ctr, 0, 8 * PI_NSTAT, c->stream));
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if ((rc = inflate_blocks(c, d, db, n, duoff, ub, st, check_crc != 0, crc))) return rc;
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
@@ -678,7 +656,6 @@ int hbam_inflate(hbam_ctx* c, const uint8_t* comp, int on_device, uint64_t comp_
   c->timing.resolve_ms = ev_ms(c, 11, 1);
   c->timing.n_blocks = n;
   c->timing.ubuf_bytes = uo[n];
-  HIPCHK(c, copy_sync(c, &c->timing.n_retry, c->retry_ctr, 8, hipMemcpyDeviceToHost));
   for (uint64_t i = 0; i < n; ++i) {
     int32_t s = hst[i] == INF_OK ? HBAM_OK : hst[i] == INF_SHORT ? HBAM_EFORMAT : HBAM_EDATA;
     if (s == HBAM_OK && check_crc && hcrc[i] != hb[i].crc) s = HBAM_EFORMAT;
@@ -803,7 +780,6 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if ((rc = ensure(c, B_UBUF, utotal + UBUF_SLACK, &ub))) return rc;
   if ((rc = ensure(c, B_INFST, nb + 1, &st))) return rc;
   if ((rc = ensure(c, B_CRC, nb + 1, &crc))) return rc;
-  HIPCHK(c, hipMemsetAsync(c->retry_ctr, 0, 8 * PI_NSTAT, c->stream));
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   if ((rc = inflate_blocks(c, d, blk, nb, uoff, ub, st, c->opts.check_crc != 0, crc))) return rc;
   HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
@@ -1008,7 +984,6 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   c->timing.ubuf_bytes = utotal;
   c->timing.n_records = n_final;
   c->timing.pool_bytes = tot_name + 4 * tot_cig + 2 * tot_seq + tot_aux;
-  HIPCHK(c, copy_sync(c, &c->timing.n_retry, c->retry_ctr, 8, hipMemcpyDeviceToHost));
   return HBAM_OK;
 }
 
@@ -1455,6 +1430,44 @@ extern "C" int64_t hbam_bgzf_block_index(hbam_ctx* c, const uint8_t* file, int o
   }
   out[k] = len & 0xffffffffffffull;
   return (int64_t)(k + 1);
+}
+
+extern "C" int hbam_resolve_tokens(hbam_ctx* c, uint8_t* io, uint32_t isize, const uint32_t* bitmap,
+                                   uint32_t tail_token, uint32_t tail_dist, int32_t* status) {
+  if (!c || !io || !bitmap || !status || isize == 0 || isize > 65536u) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  BlockRec* blk;
+  uint64_t* uoff;
+  uint8_t* ub;
+  uint32_t *bm, *tails;
+  int32_t* st;
+  int rc;
+  if ((rc = ensure(c, B_BLK, 1, &blk)) || (rc = ensure(c, B_UOFF, 2, &uoff)) ||
+      (rc = ensure(c, B_UBUF, isize + UBUF_SLACK, &ub)) || (rc = ensure(c, B_BITMAP, BITMAP_WORDS, &bm)) ||
+      (rc = ensure(c, B_TAILS, 2, &tails)) || (rc = ensure(c, B_INFST, 1, &st)))
+    return rc;
+  BlockRec r{};
+  r.isize = isize;
+  r.clen = 26;
+  const uint64_t uo[2] = {0, isize};
+  const uint32_t tl[2] = {tail_token, tail_dist};
+  const int32_t zero = INF_OK;
+  HIPCHK(c, hipMemsetAsync(ub, 0, isize + UBUF_SLACK, c->stream));
+  HIPCHK(c, hipMemsetAsync(bm, 0, BITMAP_WORDS * 4, c->stream));
+  HIPCHK(c, hipMemcpyAsync(blk, &r, sizeof r, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(uoff, uo, sizeof uo, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(ub, io, isize, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(bm, bitmap, 4ull * ((isize + 31u) / 32u), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(tails, tl, sizeof tl, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(st, &zero, 4, hipMemcpyHostToDevice, c->stream));
+  k_resolve<<<1, 64, 0, c->stream>>>(blk, uoff, 1, ub, bm, tails, st);
+  HIPCHK(c, hipGetLastError());
+  int32_t hs = 0;
+  HIPCHK(c, hipMemcpyAsync(&hs, st, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(io, ub, isize, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *status = hs == INF_OK ? HBAM_OK : HBAM_EDATA;
+  return HBAM_OK;
 }
 
 #ifdef HBAM_PROF

@@ -20,7 +20,7 @@
 
 #include "hbam_internal.h"
 #include "inflate_dev.h"
-#include "inflate_par.h"
+#include "inflate_tok.h"
 #include "resolve_dev.h"
 
 namespace hbam {
@@ -134,9 +134,9 @@ __global__ void k_verify_chain(const uint8_t* __restrict__ comp, const uint64_t*
 // ------------------------------------------------------------------------------------
 // K2: inflate = two kernels.
 //  k_inflate_tokens (phase 1): one lane per BGZF block (SIMT across blocks); Huffman
-//    decode; literals land in ubuf, each match leaves a 3-byte descriptor in its hole and a
-//    bit in the block's match-start bitmap (TokenSink, inflate_dev.h).  LDS: per lane
-//    288 u16 + 32 u8 symbol slots.
+//    decode with wave-uniform input epochs; literals land in ubuf, each match leaves a
+//    3-byte descriptor in its hole and a bit in the block's match-start bitmap (TSink,
+//    inflate_tok.h).  LDS: per lane 288 + 32 u8 symbol slots.
 //  k_resolve (phase 2): one wave per block; the block's output is staged in LDS (64 KiB),
 //    matches are executed in order in batches of mutually independent copies (a match
 //    whose source ends before the first pending destination), then written back.
@@ -148,21 +148,19 @@ __device__ unsigned long long* g_prof = nullptr;
 #define PROF_CLK() __builtin_amdgcn_s_memtime()
 #define PROF_RT() __builtin_amdgcn_s_memrealtime()
 #endif
-__global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __restrict__ comp,
-                                                               const BlockRec* __restrict__ blk,
-                                                               const uint64_t* __restrict__ uoff,
-                                                               uint32_t nblk, uint8_t* __restrict__ ubuf,
-                                                               uint8_t* __restrict__ lens_scratch,
-                                                               uint32_t* __restrict__ bitmap,
-                                                               uint32_t* __restrict__ tails,
-                                                               int32_t* __restrict__ status,
-                                                               int retry_only) {
-  // 320 B of LDS per lane (u8 lit/len symbols): 20 KiB per workgroup -> 8 per CU
+__global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t* __restrict__ comp,
+                                                                  const BlockRec* __restrict__ blk,
+                                                                  const uint64_t* __restrict__ uoff,
+                                                                  uint32_t nblk, uint8_t* __restrict__ ubuf,
+                                                                  uint8_t* __restrict__ lens_scratch,
+                                                                  uint32_t* __restrict__ bitmap,
+                                                                  uint32_t* __restrict__ tails,
+                                                                  int32_t* __restrict__ status) {
+  // 320 B of LDS per lane (u8 lit/len + distance symbols): 20 KiB per workgroup -> 8 per CU
   __shared__ uint8_t s_ll[INFLATE_WG * 288];
   __shared__ uint8_t s_d[INFLATE_WG * 32];
   const uint32_t b = blockIdx.x * INFLATE_WG + threadIdx.x;
   if (b >= nblk) return;
-  if (retry_only && status[b] != INF_RETRY) return;
 #ifdef HBAM_PROF
   const uint64_t pr0 = PROF_RT(), pc0 = PROF_CLK();
 #endif
@@ -175,22 +173,11 @@ __global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __
   } else if (r.clen < 26u) {
     st = INF_DATA;  // Inflater.setInput with a negative length
   } else {
-    const uint64_t u0 = uoff[b];
-    TokenSink sink;
-    sink.ubuf = ubuf;
-    sink.start = u0;
-    sink.end = u0 + r.isize;
-    sink.cur = ~0ULL;
-    sink.lo = 0;
-    sink.hi = 0;
-    sink.bm = bitmap + (uint64_t)b * BITMAP_WORDS;
-    sink.bw = 0;
-    sink.bword = 0;
-    sink.nwords = (r.isize + 31u) >> 5;
-    sink.tail = tails + 2 * (uint64_t)b;
-    st = inflate_core(comp + r.coff + 18, r.clen - 26u, r.isize, s_ll + threadIdx.x * 288,
-                      s_d + threadIdx.x * 32, lens_scratch + (uint64_t)b * LENS_SLOT, sink,
-                      &produced);
+    TSink sink;
+    sink.init(ubuf, uoff[b], r.isize, bitmap + (uint64_t)b * BITMAP_WORDS, tails + 2 * (uint64_t)b);
+    st = inflate_tokens_block(comp + r.coff + 18, r.clen - 26u, r.isize, s_ll + threadIdx.x * 288,
+                              s_d + threadIdx.x * 32, lens_scratch + (uint64_t)b * LENS_SLOT, sink,
+                              &produced);
   }
   status[b] = st;
 #ifdef HBAM_PROF
@@ -203,53 +190,13 @@ __global__ __launch_bounds__(INFLATE_WG) void k_inflate_tokens(const uint8_t* __
 #endif
 }
 
-// Phase 1, wave-parallel (inflate_par.h): one workgroup of PI_NL lanes per block.  Blocks it
-// does not finish exactly are marked INF_RETRY for k_inflate_tokens(retry_only = 1).
-__global__ __launch_bounds__(PI_NL) void k_inflate_par(const uint8_t* __restrict__ comp,
-                                                      const BlockRec* __restrict__ blk,
-                                                      const uint64_t* __restrict__ uoff, uint32_t nblk,
-                                                      uint8_t* __restrict__ ubuf,
-                                                      uint32_t* __restrict__ bitmap,
-                                                      uint32_t* __restrict__ tails,
-                                                      int32_t* __restrict__ status,
-                                                      unsigned long long* __restrict__ n_retry) {
-  __shared__ PiShared s;
-  const uint32_t b = blockIdx.x;
-  if (b >= nblk) return;
-  const BlockRec r = blk[b];
-  int32_t st;
-  PiStat ps;
-#pragma unroll
-  for (uint32_t i = 0; i < PI_NSTAT; ++i) ps.v[i] = 0;
-  if (r.isize > 65536u) {
-    st = INF_OK;  // unsupported here; the runtime reports HBAM_EUNSUPPORTED for it
-  } else if (r.clen < 26u) {
-    st = INF_DATA;  // Inflater.setInput with a negative length
-  } else {
-    st = inflate_par_block(s, comp + r.coff + 18, r.clen - 26u, r.isize, ubuf, uoff[b], ps);
-    if (st == INF_OK) {
-      const uint32_t nwords = (r.isize + 31u) >> 5;
-      uint32_t* bm = bitmap + (uint64_t)b * BITMAP_WORDS;
-      for (uint32_t i = threadIdx.x; i < nwords; i += PI_NL) bm[i] = s.bm[i];
-    }
-  }
-  if (threadIdx.x == 0) {
-    status[b] = st;
-    tails[2 * (uint64_t)b] = 0;
-    if (st == INF_RETRY) atomicAdd(n_retry, 1ull);
-    ps.v[10] = 1;
-#pragma unroll
-    for (uint32_t i = 1; i < PI_NSTAT; ++i) atomicAdd(n_retry + i, (unsigned long long)ps.v[i]);
-  }
-}
-
 // LZ77 resolution of one block (phase 2 of the batched inflate); see resolve_dev.h.
 __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk,
                                                 const uint64_t* __restrict__ uoff, uint32_t nblk,
                                                 uint8_t* __restrict__ ubuf,
                                                 const uint32_t* __restrict__ bitmap,
                                                 const uint32_t* __restrict__ tails,
-                                                const int32_t* __restrict__ status) {
+                                                int32_t* __restrict__ status) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RS_BUF];
   __shared__ uint64_t s_rec[RS_MAXM];   // pre matches from the front, ordered from the back
   __shared__ uint16_t s_pos[RS_MAXM];
@@ -267,6 +214,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
   const uint32_t* bm = bitmap + (uint64_t)b * BITMAP_WORDS;
   const uint32_t nwords = (isize + 31u) >> 5;
   const uint32_t tail0 = tails[2 * (uint64_t)b];
+  bool tail_bad = false;
   {
     uint32_t any = 0;
     for (uint32_t w = lane; w < nwords; w += 64) any |= bm[w];
@@ -332,6 +280,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     __syncthreads();
     // ---- descriptors -> records, split pre / ordered
     uint32_t npre = 0, nord = 0;
+    bool bad_desc = false;
     for (uint32_t j0 = 0; j0 < total; j0 += 64) {
       const uint32_t j = j0 + lane;
       uint64_t rec = 0;
@@ -345,12 +294,19 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
         rec = (uint64_t)p | (uint64_t)len << 16 | (uint64_t)dist << 32 | (uint64_t)e << 48;
         pre = e <= s0;
         ord = !pre;
+        // a descriptor the Huffman pass cannot have written (source before the block, or a
+        // hole past the block end): the block's tokens are corrupt
+        bad_desc |= dist > p || p + len > isize;
       }
       const uint64_t mp = __ballot(pre), mo = __ballot(ord);
       if (pre) s_rec[npre + lane_rank(mp)] = rec;
       if (ord) s_rec[RS_MAXM - 1 - (nord + lane_rank(mo))] = rec;
       npre += (uint32_t)__popcll(mp);
       nord += (uint32_t)__popcll(mo);
+    }
+    if (__any(bad_desc)) {  // never copy from outside the block: report DataFormatException
+      if (lane == 0) status[b] = INF_DATA;
+      return;
     }
     __syncthreads();
 #ifdef HBAM_PROF
@@ -377,6 +333,10 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
       const bool ready = (j < nord) && (uint32_t)(rec >> 48) <= pk;
       const uint64_t nr = __ballot(!ready);
       const uint32_t c = nr ? (uint32_t)(__ffsll((unsigned long long)nr) - 1) : 64u;
+      if (c == 0u) {  // no progress possible (validated descriptors always make some): corrupt
+        if (lane == 0) status[b] = INF_DATA;
+        return;
+      }
       if (lane < c) {
         const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
                        dist = (uint32_t)(rec >> 32) & 0xffffu;
@@ -390,9 +350,14 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     if ((tail0 & 0x80000000u) && (tail0 & 0xffffu) / RS_S == k && lane == 0) {
       // final match shorter than 3 bytes (the output filled up inside it); last token
       const uint32_t p = tail0 & 0xffffu, n = (tail0 >> 16) & 0x7fffu;
-      const uint32_t d = tails[2 * (uint64_t)b + 1];
+      uint32_t d = tails[2 * (uint64_t)b + 1];
+      if (d == 0u || d > p || p + n > isize) {  // corrupt tail token: no copy from outside
+        status[b] = INF_DATA;
+        d = 1u;
+        tail_bad = true;
+      }
       uint32_t jj = 0;
-      for (uint32_t t = 0; t < n; ++t) {
+      for (uint32_t t = 0; t < n && !tail_bad; ++t) {
         const uint32_t x = p - d + jj;
         s_buf[lbase + p + t] = (x + RS_W >= s0) ? s_buf[lbase + x] : ubuf[base + x];
         jj = (jj + 1u == d) ? 0u : jj + 1u;
@@ -417,9 +382,11 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
         }
       }
     }
+    // move [RS_S, RS_S + RS_W + RS_S) down to 0 in 16-byte columns; one wave, so every read of
+    // a 1 KiB step lands before that step's writes (any RS_W that is a multiple of 16)
 #pragma unroll
-    for (uint32_t i = 0; i < (RS_W + RS_S) / 1024; ++i)
-      *(uint4*)(s_buf + 1024u * i + 16u * lane) = *(const uint4*)(s_buf + RS_S + 1024u * i + 16u * lane);
+    for (uint32_t o = 16u * lane; o < RS_W + RS_S; o += 1024u)
+      *(uint4*)(s_buf + o) = *(const uint4*)(s_buf + RS_S + o);
     *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = ra0;
     if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = ra1;
     load_raw(k + 3, ra0, ra1);

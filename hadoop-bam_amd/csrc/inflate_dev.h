@@ -290,8 +290,15 @@ struct TokenSink {
   uint32_t bw, bword, nwords;
   uint32_t* tail;   // [0] = op | n<<16 | 1<<31 for a final match shorter than 3 bytes, [1] = dist
 
+#ifdef HBAM_AB_NOSTORE
+  uint64_t ab_acc = 0;  // A/B build only: output stores replaced by a register fold
+#endif
   __device__ __forceinline__ void flush() {
     if (cur == ~0ULL) return;
+#ifdef HBAM_AB_NOSTORE
+    ab_acc ^= lo ^ (hi << 1) ^ cur;
+    return;
+#endif
     if (cur >= start && cur + 16 <= end) {
       uint4 v;
       v.x = (uint32_t)lo; v.y = (uint32_t)(lo >> 32); v.z = (uint32_t)hi; v.w = (uint32_t)(hi >> 32);
@@ -319,7 +326,11 @@ struct TokenSink {
   __device__ __forceinline__ void mark(uint32_t op) {
     const uint32_t w = op >> 5;
     while (bw < w) {
+#ifdef HBAM_AB_NOSTORE
+      ab_acc += bword;
+#else
       st_out(bm + bw, bword);
+#endif
       bword = 0;
       ++bw;
     }
@@ -340,6 +351,10 @@ struct TokenSink {
   }
   __device__ __forceinline__ void finish(uint32_t) {
     flush();
+#ifdef HBAM_AB_NOSTORE
+    if (end > start) ubuf[start] = (uint8_t)(ab_acc ^ (ab_acc >> 8) ^ (ab_acc >> 40));
+    return;
+#endif
     while (bw < nwords) {
       st_out(bm + bw, bword);
       bword = 0;

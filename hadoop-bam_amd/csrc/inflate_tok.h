@@ -1,0 +1,539 @@
+// inflate_tok.h — Huffman pass of the batched BGZF inflate (k_inflate_tokens), gfx950.
+//
+// Replaces [htsjdk] BlockGunzipper.unzipBlock -> java.util.zip.Inflater (JDK zlib) on the BAM
+// read path; the observable contract is zlib 1.2.11's as documented in inflate_dev.h (ONE
+// inflate(Z_PARTIAL_FLUSH) call with avail_out = ISIZE; identical error conditions).
+//
+// One lane decodes one BGZF block (SIMT over 64 blocks per wave).  What makes a lane-per-
+// block decoder slow on CDNA is not the bit arithmetic but memory waits: a per-lane refill
+// that loads the next 16 compressed bytes when the lane runs dry puts an
+// `s_waitcnt vmcnt(...)` on the critical path of EVERY loop iteration, because some lane of
+// the 64 is always refilling and the wait is per wave.  Here the input moves in wave-uniform
+// epochs instead:
+//   * each lane holds 32 compressed bytes in two register banks plus a 64-bit bit buffer;
+//   * every HBAM_TOK_K iterations (the same iteration for every active lane) a lane merges
+//     the 16-byte quad it requested at the previous epoch into a free bank and requests the
+//     next one, so a load has a whole epoch to land before anything waits on it;
+//   * a lane that would need more bits than its banks hold skips the iteration (stall) until
+//     the next epoch, which only happens on runs of long, far matches.
+// Output (TSink): literals at their final ubuf offsets, a 3-byte descriptor (len-3, dist-1)
+// at the start of every match hole, one bitmap bit per match start (128-position windows
+// written as 16-byte stores), a 16-byte register write-combine chunk for the bytes.
+// k_resolve (resolve_dev.h) then fills the holes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "inflate_dev.h"
+
+namespace hbam {
+
+#ifndef HBAM_TOK_K
+#define HBAM_TOK_K 4  // symbol-loop iterations per input epoch (power of two)
+#endif
+constexpr uint32_t TOK_K = HBAM_TOK_K;
+constexpr uint32_t TOK_LENS_LL = 32;    // lens scratch: lit/len code lengths at +32 ..
+constexpr uint32_t TOK_LENS_D = 320;    //               distance code lengths at +320 (<= 30)
+
+// ---- input: two register banks + one quad in flight ------------------------------------
+typedef const __attribute__((address_space(1))) u32x4_t* gq_ptr;  // global (not flat) loads
+__device__ __forceinline__ u32x4_t ein_load(const uint4* p) { return *(gq_ptr)p; }
+struct EIn {
+  const uint4* fp;    // quad held in t (merged at the next epoch); == fend when the fetch is done
+  const uint4* fend;  // one past the last quad that holds stream bytes
+  const uint4* safe;  // an address already read (target of the dummy load after the fetch)
+  uint4 q0, q1;       // banks: stream dwords, ring positions 0..3 and 4..7
+  u32x4_t t;          // quad requested at the last epoch
+  uint32_t rd;        // next ring position to move into bb
+  uint32_t nv;        // unread dwords in the banks (from rd)
+  uint64_t bb;        // bit buffer, LSB first
+  uint32_t bc;        // valid bits in bb
+  uint32_t consumed;  // stream bits consumed
+  uint32_t total;     // 8 * deflated bytes
+};
+
+// (component-wise selects: a select between two uint4 lvalues becomes a select between their
+// addresses, which pins the whole reader in scratch)
+__device__ __forceinline__ uint32_t ein_sel(const EIn& e, uint32_t i) {
+  const bool h = (i & 4u) != 0u, z = (i & 2u) != 0u;
+  const uint32_t x = h ? e.q1.x : e.q0.x, y = h ? e.q1.y : e.q0.y;
+  const uint32_t zz = h ? e.q1.z : e.q0.z, w = h ? e.q1.w : e.q0.w;
+  const uint32_t a = z ? zz : x, b = z ? w : y;
+  return (i & 1u) ? b : a;
+}
+__device__ __forceinline__ void ein_init(EIn& e, const uint8_t* p, uint32_t nbytes) {
+  const uintptr_t a = (uintptr_t)p & 15u;
+  const uint4* base = (const uint4*)(p - a);
+  e.fend = (const uint4*)(((uintptr_t)(p + nbytes) + 15u) & ~(uintptr_t)15u);
+  e.safe = base;
+  e.q0 = base[0];
+  e.q1 = base[1];
+  e.fp = base + 2;
+  if (e.fp > e.fend) e.fp = e.fend;
+  e.t = ein_load(e.fp < e.fend ? e.fp : e.safe);
+  const uint32_t r = (uint32_t)(a >> 2);
+  const uint32_t sh = 8u * (uint32_t)(a & 3u);
+  e.bb = (uint64_t)(ein_sel(e, r) >> sh);
+  e.bc = 32u - sh;
+  e.rd = r + 1u;
+  e.nv = 8u - e.rd;
+  e.consumed = 0;
+  e.total = nbytes * 8u;
+}
+// one dword from the banks into bb (the stall check guarantees the banks hold what is needed)
+__device__ __forceinline__ void ein_refill(EIn& e) {
+  if (e.bc <= 32u && e.nv != 0u) {
+    e.bb |= (uint64_t)ein_sel(e, e.rd) << e.bc;
+    e.bc += 32u;
+    e.rd = (e.rd + 1u) & 7u;
+    --e.nv;
+  }
+}
+// epoch boundary: merge the quad in flight into the free bank, request the next one
+__device__ __forceinline__ void ein_epoch(EIn& e) {
+  if (e.fp < e.fend && e.nv <= 4u) {
+    const bool hi = (((e.rd + e.nv) & 7u) >> 2) != 0u;
+    const u32x4_t t = e.t;
+    e.q0.x = hi ? e.q0.x : t[0];
+    e.q0.y = hi ? e.q0.y : t[1];
+    e.q0.z = hi ? e.q0.z : t[2];
+    e.q0.w = hi ? e.q0.w : t[3];
+    e.q1.x = hi ? t[0] : e.q1.x;
+    e.q1.y = hi ? t[1] : e.q1.y;
+    e.q1.z = hi ? t[2] : e.q1.z;
+    e.q1.w = hi ? t[3] : e.q1.w;
+    e.nv += 4u;
+    ++e.fp;
+  }
+  e.t = ein_load(e.fp < e.fend ? e.fp : e.safe);
+}
+// bits the lane can use without another epoch
+__device__ __forceinline__ bool ein_short(const EIn& e, uint32_t need) {
+  return e.bc + 32u * e.nv < need && e.fp < e.fend;
+}
+// synchronous top-up (header phase): epochs until `need` bits are buffered or the fetch is done
+__device__ __forceinline__ void ein_ensure(EIn& e, uint32_t need) {
+  while (ein_short(e, need)) ein_epoch(e);
+  ein_refill(e);
+  ein_refill(e);
+}
+__device__ __forceinline__ uint32_t ein_avail(const EIn& e) { return e.total - e.consumed; }
+__device__ __forceinline__ uint32_t ein_peek(const EIn& e, uint32_t n) {
+  return (uint32_t)e.bb & ((1u << n) - 1u);
+}
+__device__ __forceinline__ void ein_drop(EIn& e, uint32_t n) {
+  e.bb >>= n;
+  e.bc -= n;
+  e.consumed += n;
+}
+__device__ __forceinline__ uint32_t ein_rev15(const EIn& e) {
+  return __builtin_bitreverse32((uint32_t)e.bb) >> 17;
+}
+
+// ---- output ------------------------------------------------------------------------------
+struct TSink {
+  uint8_t* cbase;   // 16-aligned address of chunk 0 (the chunk holding the block's first byte)
+  uint32_t soff;    // block start inside chunk 0
+  uint32_t iend;    // soff + isize
+  uint32_t curc;    // chunk held in lo/hi (~0u = none)
+  uint64_t lo, hi;
+  uint32_t* bm;     // match-start bitmap of the block (BITMAP_WORDS words)
+  uint32_t bwin;    // 128-position window held in w0..w3
+  uint32_t nwin;    // windows covering the block
+  uint32_t w0, w1, w2, w3;
+  uint32_t* tail;   // [0] = op | n<<16 | 1<<31 for a final match shorter than 3 bytes, [1] = dist
+
+  __device__ __forceinline__ void init(uint8_t* ubuf, uint64_t start, uint32_t isize, uint32_t* bmp,
+                                       uint32_t* tl) {
+    cbase = ubuf + (start & ~15ull);
+    soff = (uint32_t)(start & 15u);
+    iend = soff + isize;
+    curc = ~0u;
+    lo = hi = 0;
+    bm = bmp;
+    bwin = 0;
+    nwin = (isize + 127u) >> 7;
+    w0 = w1 = w2 = w3 = 0;
+    tail = tl;
+    tail[0] = 0;
+  }
+  __device__ __forceinline__ void flush() {
+    if (curc == ~0u) return;
+    const uint32_t r0 = curc << 4;
+    if (r0 >= soff && r0 + 16u <= iend) {
+      const uint4 v = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+      st_out((uint4*)(cbase + r0), v);
+    } else {  // chunk shared with a neighbouring block: only this block's bytes
+      for (uint32_t k = 0; k < 16u; ++k) {
+        const uint32_t r = r0 + k;
+        if (r >= soff && r < iend) cbase[r] = (uint8_t)((k < 8u ? lo >> (8u * k) : hi >> (8u * (k - 8u))) & 0xffu);
+      }
+    }
+  }
+  __device__ __forceinline__ void chunk(uint32_t c) {
+    if (c != curc) {
+      flush();
+      curc = c;
+      lo = 0;
+      hi = 0;
+    }
+  }
+  __device__ __forceinline__ void win_store() {
+    st_out((uint4*)(bm + 4u * bwin), make_uint4(w0, w1, w2, w3));
+  }
+  __device__ __forceinline__ void mark(uint32_t op) {
+    const uint32_t w = op >> 7;
+    while (bwin < w) {
+      win_store();
+      w0 = w1 = w2 = w3 = 0;
+      ++bwin;
+    }
+    const uint32_t i = op & 127u, m = 1u << (i & 31u), q = i >> 5;
+    w0 |= q == 0u ? m : 0u;
+    w1 |= q == 1u ? m : 0u;
+    w2 |= q == 2u ? m : 0u;
+    w3 |= q == 3u ? m : 0u;
+  }
+  __device__ __forceinline__ void literal(uint32_t op, uint32_t b) {
+    const uint32_t r = soff + op;
+    chunk(r >> 4);
+    const uint64_t v = (uint64_t)(b & 0xffu) << ((r & 7u) << 3);
+    if (r & 8u) hi |= v;
+    else lo |= v;
+  }
+  __device__ __forceinline__ void match(uint32_t op, uint32_t n, uint32_t dist) {
+    if (n < 3u) {  // the output filled up inside the match: last token of the block
+      tail[0] = op | n << 16 | 0x80000000u;
+      tail[1] = dist;
+      return;
+    }
+    const uint64_t d = (uint64_t)((n - 3u) | (dist - 1u) << 8);  // 3 bytes
+    const uint32_t r = soff + op;
+    const uint32_t c = r >> 4, k = r & 15u;
+    chunk(c);
+    if (k < 8u) {
+      lo |= d << (8u * k);
+      if (k > 5u) hi |= d >> (64u - 8u * k);
+    } else {
+      hi |= d << (8u * (k - 8u));  // bytes past the chunk (k >= 14) fall off here ...
+    }
+    if (k >= 14u) {  // ... and start the next chunk
+      const uint64_t spill = d >> (8u * (16u - k));
+      flush();
+      curc = c + 1u;
+      lo = spill;
+      hi = 0;
+    }
+    mark(op);
+  }
+  __device__ __forceinline__ void finish() {
+    flush();
+    while (bwin < nwin) {
+      win_store();
+      w0 = w1 = w2 = w3 = 0;
+      ++bwin;
+    }
+  }
+};
+
+// ---- canonical tables from code lengths in global scratch ---------------------------------
+// lens: 16-aligned global bytes (n of them); kind 0 = code lengths, 1 = lit/len, 2 = distances.
+// The lengths are read 16 at a time, the next quad requested before the current one is
+// processed (one wait per 16 symbols instead of one per symbol).
+__device__ __forceinline__ uint32_t quad_byte(const uint4& q, uint32_t j) {  // j compile-time
+  const uint32_t w = j < 4 ? q.x : j < 8 ? q.y : j < 12 ? q.z : q.w;
+  return (w >> (8u * (j & 3u))) & 0xffu;
+}
+// Out of line: called once per DEFLATE block, and inlining its unrolled counters into the
+// kernel pushes the symbol loop's state into scratch.
+__device__ __attribute__((noinline)) bool tok_build(const uint8_t* __restrict__ lens, int n,
+                                                    uint8_t* __restrict__ syms, Huff& h, int kind) {
+  typedef uint8_t SymT;
+  const uint4* lq = (const uint4*)lens;
+  const int nq = (n + 15) >> 4;
+  uint32_t cnt[16], nhi[16];
+#pragma unroll
+  for (int L = 0; L < 16; ++L) cnt[L] = nhi[L] = 0;
+  uint4 qn = lq[0];
+  for (int k = 0; k < nq; ++k) {
+    const uint4 q = qn;
+    if (k + 1 < nq) qn = lq[k + 1];
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const int s = 16 * k + (int)j;
+      const uint32_t len = s < n ? quad_byte(q, j) : 0u;
+      const uint32_t hb = (kind == 1 && s >= 256) ? 1u : 0u;
+#pragma unroll
+      for (int L = 1; L < 16; ++L) {
+        cnt[L] += (len == (uint32_t)L) ? 1u : 0u;
+        nhi[L] += (len == (uint32_t)L) ? hb : 0u;
+      }
+    }
+  }
+  uint32_t maxl = 0;
+#pragma unroll
+  for (int L = 1; L < 16; ++L) maxl = cnt[L] ? (uint32_t)L : maxl;
+  h.empty = (maxl == 0);
+  if (maxl != 0) {
+    int32_t left = 1;
+    bool over = false;
+#pragma unroll
+    for (int L = 1; L < 16; ++L) {
+      left = 2 * left - (int32_t)cnt[L];
+      over |= left < 0;
+    }
+    if (over) return false;
+    if (left > 0 && (kind == 0 || maxl != 1)) return false;  // incomplete set
+  }
+  uint32_t code = 0, base = 0;
+  uint32_t next[16];
+  int32_t prev_off = 0;
+#pragma unroll
+  for (int L = 1; L < 16; ++L) {
+    h.lim[L - 1] = (code + cnt[L]) << (15 - L);
+    h.hlim[L - 1] = (code + cnt[L] - nhi[L]) << (15 - L);
+    const int32_t off = (int32_t)base - (int32_t)code;
+    h.doff[L - 1] = off - prev_off;
+    prev_off = off;
+    next[L] = base;
+    base += cnt[L];
+    code = (code + cnt[L]) << 1;
+  }
+  if (maxl == 0) {
+#pragma unroll
+    for (int L = 0; L < 15; ++L) h.lim[L] = h.hlim[L] = 0;
+  }
+  qn = lq[0];
+  for (int k = 0; k < nq; ++k) {
+    const uint4 q = qn;
+    if (k + 1 < nq) qn = lq[k + 1];
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const int s = 16 * k + (int)j;
+      const uint32_t len = s < n ? quad_byte(q, j) : 0u;
+      if (len) {
+        uint32_t pos = 0;
+#pragma unroll
+        for (int L = 1; L < 16; ++L) {
+          const bool eq = (len == (uint32_t)L);
+          pos = eq ? next[L] : pos;
+          next[L] += eq ? 1u : 0u;
+        }
+        syms[pos] = (SymT)s;
+      }
+    }
+  }
+  return true;
+}
+
+// Inflate one raw DEFLATE stream (cdata, nbytes) to exactly isize bytes into the token sink.
+// syms_ll: 288 u8 LDS slots (symbol & 255; bit 8 from Huff.hlim); syms_d: 32 u8 LDS slots;
+// lens: LENS_SLOT bytes of 16-aligned global scratch.  Returns INF_OK / INF_SHORT / INF_DATA.
+__device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restrict__ cdata, uint32_t nbytes,
+                                        uint32_t isize, uint8_t* __restrict__ syms_ll,
+                                        uint8_t* __restrict__ syms_d, uint8_t* __restrict__ lens,
+                                        TSink& sink, uint32_t* produced) {
+  EIn in;
+  ein_init(in, cdata, nbytes);
+  uint32_t op = 0;
+  Huff hl, hd;
+  bool last = false;
+  int32_t rc = INF_OK;
+  uint32_t it = 0;  // iteration counter shared by the lanes of a phase (epoch clock)
+  for (;;) {
+    if (last) break;  // stream end
+    ein_ensure(in, 64);
+    if (ein_avail(in) < 3u) goto leave;
+    last = (in.bb & 1u) != 0;
+    {
+      const uint32_t type = (uint32_t)(in.bb >> 1) & 3u;
+      ein_drop(in, 3);
+      if (type == 0u) {
+        // stored: byte align, LEN/NLEN, then LEN literal bytes
+        const uint32_t pad = (8u - (in.consumed & 7u)) & 7u;
+        ein_drop(in, pad);
+        ein_ensure(in, 64);
+        if (ein_avail(in) < 32u) goto leave;
+        const uint32_t w = (uint32_t)in.bb;
+        if ((w & 0xffffu) != ((w >> 16) ^ 0xffffu)) { rc = INF_DATA; goto done; }
+        ein_drop(in, 32);
+        uint32_t len = w & 0xffffu;
+        for (; len; --len) {
+          if (op == isize) goto leave;
+          if ((++it & (TOK_K - 1u)) == 0u) ein_epoch(in);
+          if (ein_short(in, 8)) { ++len; continue; }  // stall: retry this byte next epoch
+          ein_refill(in);
+          if (ein_avail(in) < 8u) goto leave;
+          sink.literal(op++, (uint32_t)in.bb & 0xffu);
+          ein_drop(in, 8);
+        }
+        continue;
+      } else if (type == 1u) {
+        // fixed Huffman code: lengths 8/9/7/8 for lit/len, 5 for distances
+        uint32_t* l32 = (uint32_t*)(lens + TOK_LENS_LL);
+        for (int s = 0; s < 288; s += 4) {
+          const uint32_t v = s < 144 ? 8u : s < 256 ? 9u : s < 280 ? 7u : 8u;
+          l32[s / 4] = v * 0x01010101u;
+        }
+        uint32_t* d32 = (uint32_t*)(lens + TOK_LENS_D);
+        for (int s = 0; s < 32; s += 4) d32[s / 4] = 0x05050505u;
+        Huff t;
+        tok_build(lens + TOK_LENS_LL, 288, syms_ll, t, 1);
+        hl = t;
+        tok_build(lens + TOK_LENS_D, 32, syms_d, t, 2);
+        hd = t;
+      } else if (type == 2u) {
+        ein_ensure(in, 64);
+        if (ein_avail(in) < 14u) goto leave;
+        const uint32_t nlen = ((uint32_t)in.bb & 31u) + 257u;
+        const uint32_t ndist = ((uint32_t)(in.bb >> 5) & 31u) + 1u;
+        const uint32_t ncode = ((uint32_t)(in.bb >> 10) & 15u) + 4u;
+        ein_drop(in, 14);
+        if (nlen > 286u || ndist > 30u) { rc = INF_DATA; goto done; }
+        // 19 code-length code lengths (3 bits each, RFC 1951 order), at lens[0..19)
+        const uint64_t ord_lo = 0x022caa324e804a30ULL, ord_hi = 0x00000003c2e1346cULL;
+        {
+          uint4* l4 = (uint4*)lens;
+          l4[0] = make_uint4(0, 0, 0, 0);
+          l4[1] = make_uint4(0, 0, 0, 0);
+        }
+        ein_ensure(in, 64);  // 19 * 3 = 57 bits at most
+        for (uint32_t i = 0; i < ncode; ++i) {
+          ein_refill(in);
+          if (ein_avail(in) < 3u) goto leave;
+          const uint32_t o = (uint32_t)((i < 12u ? ord_lo >> (5u * i) : ord_hi >> (5u * (i - 12u))) & 31u);
+          lens[o] = (uint8_t)(in.bb & 7u);
+          ein_drop(in, 3);
+        }
+        Huff hc;
+        {
+          Huff t;  // the build writes through a pointer; the decoder keeps its copy in registers
+          if (!tok_build(lens, 19, syms_ll, t, 0)) { rc = INF_DATA; goto done; }
+          hc = t;
+        }
+        // lit/len lengths -> lens[32 ..], distance lengths -> lens[320 ..]
+        const uint32_t total = nlen + ndist;
+        uint32_t have = 0;
+        uint32_t prev = 0;
+        while (have < total) {
+          if ((++it & (TOK_K - 1u)) == 0u) ein_epoch(in);
+          if (ein_short(in, 14)) continue;  // stall
+          ein_refill(in);
+          uint32_t L, sym;
+          if (hc.empty) {
+            L = 1;
+            sym = 0;
+            if (ein_avail(in) < 1u) goto leave;
+          } else {
+            int32_t idx;
+            const uint32_t v = ein_rev15(in);
+            huff_lookup(hc, v, L, idx);  // CODES sets are complete
+            if (L > ein_avail(in)) goto leave;
+            sym = syms_ll[idx];
+          }
+          if (sym < 16u) {
+            ein_drop(in, L);
+            lens[have < nlen ? TOK_LENS_LL + have : TOK_LENS_D + (have - nlen)] = (uint8_t)sym;
+            ++have;
+            prev = sym;
+            continue;
+          }
+          const uint32_t xb = sym == 16u ? 2u : sym == 17u ? 3u : 7u;
+          if (L + xb > ein_avail(in)) goto leave;
+          ein_drop(in, L);
+          uint32_t rep;
+          uint32_t v8 = 0;
+          if (sym == 16u) {
+            if (have == 0) { rc = INF_DATA; goto done; }
+            v8 = prev;
+            rep = 3u + ein_peek(in, 2);
+          } else if (sym == 17u) {
+            rep = 3u + ein_peek(in, 3);
+          } else {
+            rep = 11u + ein_peek(in, 7);
+          }
+          ein_drop(in, xb);
+          if (have + rep > total) { rc = INF_DATA; goto done; }
+          for (uint32_t k = 0; k < rep; ++k, ++have)
+            lens[have < nlen ? TOK_LENS_LL + have : TOK_LENS_D + (have - nlen)] = (uint8_t)v8;
+          prev = v8;
+        }
+        if (lens[TOK_LENS_LL + 256] == 0) { rc = INF_DATA; goto done; }
+        {
+          Huff t;
+          if (!tok_build(lens + TOK_LENS_LL, (int)nlen, syms_ll, t, 1)) { rc = INF_DATA; goto done; }
+          hl = t;
+          if (!tok_build(lens + TOK_LENS_D, (int)ndist, syms_d, t, 2)) { rc = INF_DATA; goto done; }
+          hd = t;
+        }
+      } else {
+        rc = INF_DATA;  // invalid block type
+        goto done;
+      }
+    }
+    // Drain the table copies (scratch) before the symbol loop: otherwise the loop carries
+    // `s_waitcnt vmcnt(n)` on the distance tables into every iteration, which also waits for
+    // the iteration's own output stores.
+    __builtin_amdgcn_s_waitcnt(0);
+    // ---- symbols of a Huffman-coded block
+    for (;;) {
+      if ((++it & (TOK_K - 1u)) == 0u) ein_epoch(in);
+      if (ein_short(in, 48)) continue;  // stall until the next epoch merges more input
+      ein_refill(in);
+      uint32_t L, hi = 0;
+      int32_t idx;
+      const uint32_t v = ein_rev15(in);
+      const bool ok = huff_lookup_hi(hl, v, L, idx, hi);
+      if (!ok) {
+        if (ein_avail(in) >= 1u) { rc = INF_DATA; goto done; }
+        goto leave;
+      }
+      if (L > ein_avail(in)) goto leave;
+      const uint32_t sym = (uint32_t)syms_ll[idx] | hi;
+      ein_drop(in, L);
+      if (sym < 256u) {
+        if (op == isize) goto leave;
+        sink.literal(op++, sym);
+        continue;
+      }
+      if (sym == 256u) break;  // end of block
+      if (sym > 285u) { rc = INF_DATA; goto done; }
+      uint32_t lbase, lext;
+      length_base(sym, lbase, lext);
+      if (lext > ein_avail(in)) goto leave;
+      const uint32_t mlen = lbase + ein_peek(in, lext);
+      ein_drop(in, lext);
+      ein_refill(in);
+      const uint32_t vd = ein_rev15(in);
+      const bool okd = huff_lookup(hd, vd, L, idx);
+      if (!okd) {
+        if (ein_avail(in) >= 1u) { rc = INF_DATA; goto done; }
+        goto leave;
+      }
+      if (L > ein_avail(in)) goto leave;
+      const uint32_t dsym = syms_d[idx];
+      ein_drop(in, L);
+      if (dsym > 29u) { rc = INF_DATA; goto done; }
+      uint32_t dbase, dext;
+      dist_base(dsym, dbase, dext);
+      if (dext > ein_avail(in)) goto leave;
+      const uint32_t dist = dbase + ein_peek(in, dext);
+      ein_drop(in, dext);
+      if (op == isize) goto leave;
+      if (dist > op) { rc = INF_DATA; goto done; }
+      uint32_t n = isize - op;
+      n = mlen < n ? mlen : n;
+      sink.match(op, n, dist);
+      op += n;
+      if (n < mlen) goto leave;
+    }
+  }
+leave:
+  rc = (op == isize) ? INF_OK : INF_SHORT;
+done:
+  sink.finish();
+  *produced = op;
+  return rc;
+}
+
+}  // namespace hbam

@@ -33,7 +33,8 @@ constexpr uint32_t RS_S = HBAM_RS_S;                  // stretch (output bytes):
 constexpr uint32_t RS_C = RS_S / 1024;                // 16-byte columns per lane per stretch
 constexpr uint32_t RS_W = HBAM_RS_W;                  // window kept in LDS behind the stretch
 constexpr uint32_t RS_BUF = RS_W + 2 * RS_S + 48;     // + pad for 32-byte over-reads
-static_assert(RS_W >= RS_S && RS_W % RS_S == 0, "window must hold whole stretches (W=512 < S hung on MI355X)");
+static_assert(RS_W >= 16 && RS_W % 16 == 0 && (RS_S == 1024 || RS_S == 2048),
+              "window: whole 16-byte columns; stretch: 1 or 2 KiB (one or two columns per lane)");
 constexpr uint32_t RS_MAXM = RS_S / 3 + 2;            // matches starting in one stretch
 
 __device__ __forceinline__ uint64_t lds_rd64(const uint8_t* p) { return *(const uint64_t*)p; }

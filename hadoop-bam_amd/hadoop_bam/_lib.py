@@ -39,13 +39,12 @@ CODE_NAMES = {
 # every entry point include/hbam.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "hbam_create", "hbam_destroy", "hbam_last_error", "hbam_stream", "hbam_get_timing",
-    "hbam_inflate_stats",
     "hbam_upload", "hbam_device_free", "hbam_parse_header", "hbam_scan_blocks", "hbam_inflate",
     "hbam_decode_split", "hbam_columns_to_host", "hbam_free_host_columns",
     "hbam_release_columns", "hbam_guess_bam_record_start", "hbam_guess_batch",
     "hbam_guess_bgzf_block_start", "hbam_probabilistic_splits",
     "hbam_sort_keys", "hbam_gather_records", "hbam_permute", "hbam_splitting_index",
-    "hbam_bgzf_block_index",
+    "hbam_bgzf_block_index", "hbam_resolve_tokens",
 ]
 
 
@@ -55,7 +54,7 @@ class HbamUnavailable(RuntimeError):
 
 class Opts(C.Structure):
     _fields_ = [("check_crc", C.c_int32), ("validate_refs", C.c_int32),
-                ("inflate_mode", C.c_int32), ("reserved", C.c_int32 * 13)]
+                ("reserved", C.c_int32 * 14)]
 
 
 class Header(C.Structure):
@@ -73,7 +72,7 @@ class Timing(C.Structure):
                                           "decode_ms", "pools_ms", "total_ms",
                                           "huffman_ms", "resolve_ms")] + \
                [(n, C.c_uint64) for n in ("n_blocks", "comp_bytes", "ubuf_bytes", "n_records",
-                                          "pool_bytes", "n_retry")]
+                                          "pool_bytes", "reserved")]
 
 
 _u8p = C.POINTER(C.c_uint8)
@@ -123,7 +122,6 @@ def load(path=None):
         "hbam_last_error": (C.c_char_p, [vp]),
         "hbam_stream": (vp, [vp]),
         "hbam_get_timing": (C.c_int, [vp, C.POINTER(Timing)]),
-        "hbam_inflate_stats": (C.c_int, [vp, vp, C.c_uint32]),
         "hbam_upload": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(vp)]),
         "hbam_device_free": (C.c_int, [vp, vp]),
         "hbam_parse_header": (C.c_int, [vp, vp, C.c_int, C.c_uint64, C.POINTER(Header)]),
@@ -152,6 +150,7 @@ def load(path=None):
                                              C.c_uint64]),
         "hbam_bgzf_block_index": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_int32, vp,
                                               C.c_uint64]),
+        "hbam_resolve_tokens": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, C.c_uint32, _i32p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -184,7 +183,7 @@ def host_columns_to_numpy(h):
 class Context:
     """One device context (hbam_ctx): a HIP stream plus device work buffers."""
 
-    def __init__(self, device=0, check_crc=False, validate_refs=True, inflate_mode=0):
+    def __init__(self, device=0, check_crc=False, validate_refs=True):
         self.L = load()
         # PyTorch-ROCm ships its own HIP runtime; when both live in one process, torch's must
         # open the device first (the other order leaves torch with "No HIP GPUs").
@@ -195,7 +194,6 @@ class Context:
         o = Opts()
         o.check_crc = int(check_crc)
         o.validate_refs = int(validate_refs)
-        o.inflate_mode = int(inflate_mode)
         self.h = self.L.hbam_create(device, C.byref(o))
         if not self.h:
             raise HbamUnavailable("hbam_create failed: no HIP device %d" % device)
@@ -218,14 +216,6 @@ class Context:
         t = Timing()
         self.L.hbam_get_timing(self.h, C.byref(t))
         return {n: getattr(t, n) for n, _ in Timing._fields_}
-
-    STAT_NAMES = ["retry", "rounds", "headers", "sync_fail", "eob_overflow", "cyc_header",
-                  "cyc_pass1", "cyc_sync", "cyc_plan", "cyc_pass2", "blocks", "lanes", "commit_lane"]
-
-    def inflate_stats(self):
-        a = np.zeros(len(self.STAT_NAMES), np.uint64)
-        n = self.L.hbam_inflate_stats(self.h, C.c_void_p(a.ctypes.data), len(a))
-        return {k: int(a[i]) for i, k in enumerate(self.STAT_NAMES[:max(n, 0)])}
 
     @staticmethod
     def _ptr(data):
@@ -359,6 +349,15 @@ class Context:
         if r < 0:
             return int(r), None
         return 0, out[:r]
+
+    def resolve_tokens(self, tokens, bitmap, tail_token=0, tail_dist=0):
+        """Diagnostic: run the LZ77 pass on one token block -> (rc, status, resolved bytes)."""
+        io = np.ascontiguousarray(np.frombuffer(bytes(tokens), np.uint8)).copy()
+        bm = np.ascontiguousarray(bitmap, np.uint32)
+        st = C.c_int32(0)
+        rc = self.L.hbam_resolve_tokens(self.h, io.ctypes.data, len(io), bm.ctypes.data,
+                                        tail_token, tail_dist, C.byref(st))
+        return rc, st.value, io.tobytes()
 
     def bgzf_block_index(self, data, granularity=1):
         """BGZFBlockIndexer.index (util/BGZFBlockIndexer.java:97-181) on the device ->

@@ -57,6 +57,12 @@ class HipSortOps:
         self.L = ctx.L
         self.dev = torch.device("cuda", torch.cuda.current_device())
 
+    def _after_torch(self):
+        """libhbam runs on its own non-blocking HIP stream; tensors torch produced (an RCCL
+        all_to_all, an asynchronous copy) are complete only on torch's current stream.  Every
+        entry point below that hands torch tensors to libhbam waits for that stream first."""
+        self.torch.cuda.current_stream().synchronize()
+
     def _chk(self, rc, what):
         if rc != 0:
             raise RuntimeError("%s failed (%d): %s" % (what, rc, self.ctx.last_error()))
@@ -65,7 +71,7 @@ class HipSortOps:
         t = self.torch
         keys_out = t.empty(n, dtype=t.int64, device=self.dev)
         perm = t.empty(max(n, 1), dtype=t.int32, device=self.dev)
-        t.cuda.current_stream().synchronize()
+        self._after_torch()
         self._chk(self.L.hbam_sort_keys(self.ctx.h, C.c_void_p(key_ptr), n,
                                         C.c_void_p(keys_out.data_ptr()), C.c_void_p(perm.data_ptr())),
                   "hbam_sort_keys")
@@ -74,6 +80,7 @@ class HipSortOps:
     def _permute(self, src_ptr, elem, perm, n):
         t = self.torch
         out = t.empty(n, dtype=t.int64 if elem == 8 else t.int32, device=self.dev)
+        self._after_torch()
         self._chk(self.L.hbam_permute(self.ctx.h, C.c_void_p(src_ptr), elem, C.c_void_p(perm.data_ptr()),
                                       n, C.c_void_p(out.data_ptr())), "hbam_permute")
         return out
@@ -81,6 +88,7 @@ class HipSortOps:
     def _gather(self, ubuf_ptr, rec_off_ptr, bs_ptr, perm_ptr, n, size_only=False):
         t = self.torch
         off = t.empty(n + 1, dtype=t.int64, device=self.dev)
+        self._after_torch()
         tot = C.c_uint64(0)
         self._chk(self.L.hbam_gather_records(self.ctx.h, C.c_void_p(ubuf_ptr), C.c_void_p(rec_off_ptr),
                                              C.c_void_p(bs_ptr), C.c_void_p(perm_ptr), n, None, 0,

@@ -57,9 +57,7 @@ typedef struct hbam_ctx hbam_ctx;
 typedef struct hbam_opts {
   int32_t check_crc;
   int32_t validate_refs;
-  int32_t inflate_mode; /* 0 = lane-per-block Huffman pass (default, faster on MI355X);
-                           1 = wave-parallel Huffman pass with lane-per-block retry */
-  int32_t reserved[13];
+  int32_t reserved[14];  /* must be zero */
 } hbam_opts;
 
 typedef struct hbam_header {
@@ -118,10 +116,9 @@ typedef struct hbam_columns {
  * stream), for the roofline report. */
 typedef struct hbam_timing {
   double scan_ms, inflate_ms, crc_ms, walk_ms, decode_ms, pools_ms, total_ms;
-  double huffman_ms, resolve_ms; /* inflate = Huffman pass (k_inflate_par [+ k_inflate_tokens
-                                    for retried blocks]) + k_resolve (LZ77) */
+  double huffman_ms, resolve_ms; /* inflate = Huffman pass (k_inflate_tokens) + k_resolve (LZ77) */
   uint64_t n_blocks, comp_bytes, ubuf_bytes, n_records, pool_bytes;
-  uint64_t n_retry; /* blocks the wave-parallel Huffman pass handed to the lane-per-block one */
+  uint64_t reserved;
 } hbam_timing;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -130,11 +127,6 @@ void hbam_destroy(hbam_ctx* ctx);
 const char* hbam_last_error(const hbam_ctx* ctx);
 void* hbam_stream(hbam_ctx* ctx); /* hipStream_t of the context */
 int hbam_get_timing(const hbam_ctx* ctx, hbam_timing* out);
-/* Counters of the last inflate's wave-parallel Huffman pass (diagnostics, no reference
- * counterpart): retried blocks, rounds, DEFLATE headers, sync-failure / EOB-overflow commits,
- * shader cycles per phase (header, pass 1, sync, plan, pass 2), blocks, active lanes, commit
- * lanes.  Copies min(n, 13) values; returns that count. */
-int hbam_inflate_stats(hbam_ctx* ctx, uint64_t* out, uint32_t n);
 
 /* ---- device staging (the Java shim maps HDFS bytes into pinned buffers) ---------- */
 int hbam_upload(hbam_ctx* ctx, const uint8_t* host, uint64_t len, uint8_t** dev_out);
@@ -227,6 +219,17 @@ int64_t hbam_bgzf_block_index(hbam_ctx* ctx, const uint8_t* file, int on_device,
  * block_size) through a sort permutation. */
 int hbam_permute(hbam_ctx* ctx, const void* src, uint32_t elem_size, const uint32_t* perm,
                  uint64_t n, void* out);
+
+/* ---- diagnostics (no reference counterpart) -----------------------------------------------
+ * hbam_resolve_tokens: the LZ77 pass of the batched inflate (k_resolve) over ONE caller-built
+ * token block: `io` (host, isize <= 65536 bytes) holds literal bytes with a 3-byte descriptor
+ * (len-3, dist-1 little-endian) at the start of every match hole, `bitmap` (host,
+ * ceil(isize/32) words) one bit per match start, tail_token/tail_dist the final match shorter
+ * than 3 bytes (op | n<<16 | 1<<31, or 0).  On return `io` holds the resolved bytes and
+ * *status is HBAM_OK, or HBAM_EDATA when a token points outside the block (the pass refuses
+ * such a block instead of copying from outside it). */
+int hbam_resolve_tokens(hbam_ctx* ctx, uint8_t* io, uint32_t isize, const uint32_t* bitmap,
+                        uint32_t tail_token, uint32_t tail_dist, int32_t* status);
 
 #ifdef __cplusplus
 }

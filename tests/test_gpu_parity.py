@@ -225,52 +225,6 @@ def test_large_file_properties(gpu_ctx, genbam):
     assert got["timing"]["ubuf_bytes"] > 2 * len(data)
 
 
-# ---- wave-parallel Huffman pass (inflate_par.h) ------------------------------------------
-@pytest.mark.parametrize("kw", [dict(level=5), dict(level=6, uniform_qual=1), dict(level=1),
-                                dict(level=9), dict(payload=64, level=6), dict(level=0)])
-def test_parallel_inflate_matches_zlib_and_lane_path(gpu_ctx, oracle_mod, genbam, kw):
-    """Both Huffman passes give zlib's bytes; well-formed zlib streams never need the
-    lane-per-block retry (n_retry == 0) except where the format forces it (stored blocks are
-    handled in the fast path too)."""
-    from hadoop_bam import _lib
-    data = np.asarray(genbam.generate(records=4000, seed=33, **kw))
-    ref = oracle_mod.scan_blocks(data)
-    want = b"".join(zlib.decompressobj(-15).decompress(bytes(data[int(c) + 18:int(c) + int(l) - 8]))
-                    for c, l in zip(ref["coff"], ref["clen"]))
-    par = _lib.Context(0, inflate_mode=1)
-    rc, u, off, st = par.inflate(data, ref, check_crc=True)
-    assert rc == 0 and np.all(st == 0)
-    assert u.tobytes() == want
-    assert par.timing()["n_retry"] == 0, par.timing()
-    rc2, u2, off2, st2 = gpu_ctx.inflate(data, ref, check_crc=True)
-    assert rc2 == 0 and u2.tobytes() == want
-
-
-def test_parallel_inflate_retry_path_on_corruption(oracle_mod):
-    """Corrupted blocks go through the retry path; statuses equal the oracle's."""
-    from hadoop_bam import _lib
-    gpu_ctx = _lib.Context(0, inflate_mode=1)
-    data = _load("edge_uniform_long.bam").copy()
-    ref = oracle_mod.scan_blocks(data)
-    rng = np.random.default_rng(99)
-    nb = len(ref["coff"])
-    for i in range(0, nb, 3):
-        c, l = int(ref["coff"][i]), int(ref["clen"][i])
-        if l > 60:
-            p = c + 18 + int(rng.integers(0, l - 26))
-            data[p] ^= np.uint8(1 << int(rng.integers(0, 8)))
-    rc, u, off, st = gpu_ctx.inflate(data, ref, check_crc=True)
-    assert rc == 0
-    assert gpu_ctx.timing()["n_retry"] > 0
-    codes = {0: 0, oracle_mod.OR_EFORMAT: -3, oracle_mod.OR_EDATA: -7}
-    for i in range(nb):
-        c, l = int(ref["coff"][i]), int(ref["clen"][i])
-        orc, out = oracle_mod.inflate_block(bytes(data[c:c + l]), check_crc=True)
-        assert int(st[i]) == codes[orc], (i, int(st[i]), orc)
-        if orc == 0:
-            assert u[int(off[i]):int(off[i + 1])].tobytes() == out
-
-
 # ---- SplittingBAMIndexer on the device (SURVEY.md §8 f-2) ----------------------------------
 @pytest.mark.parametrize("fname", ["small_pe.bam", "edge_uniform_long.bam", "edge_unsorted_l1.bam"])
 @pytest.mark.parametrize("g", [1, 7, 1024, 4096])
@@ -280,3 +234,63 @@ def test_splitting_index_matches_oracle(gpu_ctx, oracle_mod, fname, g):
     rc, got = gpu_ctx.splitting_index(data, g)
     assert rc == 0, gpu_ctx.last_error()
     assert np.array_equal(got, want)
+
+
+# ---- LZ77 pass on hand-built token blocks (k_resolve) ----------------------------------------
+def _tokens(tokens, isize):
+    """(bytes, bitmap) of a token block: literals as ints, matches as (len, dist)."""
+    io = bytearray(isize)
+    bm = np.zeros((isize + 31) // 32, np.uint32)
+    op = 0
+    for t in tokens:
+        if isinstance(t, int):
+            io[op] = t
+            op += 1
+        else:
+            n, d = t
+            io[op:op + 3] = bytes([n - 3, (d - 1) & 0xff, (d - 1) >> 8])
+            bm[op >> 5] |= np.uint32(1 << (op & 31))
+            op += n
+    assert op == isize
+    return bytes(io), bm
+
+
+def test_resolve_tokens_expands_matches(gpu_ctx):
+    lits = list(b"ACGTTGCA")
+    toks = lits + [(20, 8), (5, 1)] + list(b"xy") + [(258, 30)]
+    isize = len(lits) + 20 + 5 + 2 + 258
+    io, bm = _tokens(toks, isize)
+    rc, st, out = gpu_ctx.resolve_tokens(io, bm)
+    want = bytearray()
+    for t in toks:
+        if isinstance(t, int):
+            want.append(t)
+        else:
+            n, d = t
+            for _ in range(n):
+                want.append(want[-d])
+    assert rc == 0 and st == 0
+    assert out == bytes(want)
+
+
+@pytest.mark.parametrize("case", ["dist_before_block", "hole_past_end", "tail_before_block"])
+def test_resolve_forged_descriptor_is_an_error_not_a_hang(gpu_ctx, case):
+    """A descriptor the Huffman pass could not have written (source before the block start, or
+    a hole running past the block end) makes k_resolve refuse the block (HBAM_EDATA) instead of
+    copying from outside it or spinning on a batch that never becomes ready."""
+    isize = 4096
+    toks = list(range(64)) + [(100, 50)] + [0] * (isize - 164)
+    io, bm = _tokens(toks, isize)
+    io = bytearray(io)
+    tail = (0, 0)
+    if case == "dist_before_block":
+        io[64 + 1], io[64 + 2] = 0xff, 0x0f  # dist 4096 > p = 64
+    elif case == "hole_past_end":
+        p = isize - 10
+        io[p:p + 3] = bytes([200, 0, 0])      # len 203 from p: runs past isize
+        bm[p >> 5] |= np.uint32(1 << (p & 31))
+    else:
+        tail = (5 | 2 << 16 | 0x80000000, 9)  # 2 bytes at op 5 from dist 9 > 5
+    rc, st, _ = gpu_ctx.resolve_tokens(bytes(io), bm, *tail)
+    assert rc == 0
+    assert st == -7  # HBAM_EDATA

@@ -16,7 +16,6 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=float, default=256e6)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--seed", type=int, default=2)
-ap.add_argument("--mode", type=int, default=0, help="hbam_opts.inflate_mode (0 par, 1 lane)")
 ap.add_argument("--prof", action="store_true",
                 help="use libhbam_prof.so (built with -DHBAM_PROF) and print per-block cycle stats")
 a = ap.parse_args()
@@ -28,7 +27,7 @@ d = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
 d[:len(data)].copy_(torch.from_numpy(data))
 d[len(data):].zero_()
 torch.cuda.synchronize()
-ctx = _lib.Context(0, inflate_mode=a.mode)
+ctx = _lib.Context(0)
 if a.prof:
     import ctypes as C
     L = _lib.load()
@@ -41,9 +40,6 @@ for _ in range(a.reps):
                                        h["n_ref"])
     assert rc == 0 and cols.status == 0 and cols.n_records == g.n_records
     print({k: round(v, 3) if isinstance(v, float) else v for k, v in ctx.timing().items()}, flush=True)
-    st = ctx.inflate_stats()
-    nb = max(st.get("blocks", 1), 1)
-    print("  par stats per block:", {k: round(v / nb, 2) for k, v in st.items()}, flush=True)
 
 if a.prof:
     nb = ctx.timing()["n_blocks"]
