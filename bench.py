@@ -1,18 +1,24 @@
 """Benchmark of the MI355X BAM read path (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "config #2"): a synthetic ~10 GB coordinate-sorted
-150 bp paired-end BAM (tools/gen_bam.cpp, zlib level 5, htsjdk-style packing), read as ONE
-FileVirtualSplit [first record, len<<16|0xffff] exactly as BAMRecordReader would: BGZF scan,
-inflate, record-boundary walk, fixed-field + key decode, columnar pools.  A "step" = one
-hbam_decode_split over the whole file with the compressed bytes resident in HBM.
+Workload (BASELINE.json configs[1], "config #2"): a synthetic ~10 GB coordinate-sorted 150 bp
+paired-end BAM per GPU (tools/gen_bam.cpp, zlib level 5, htsjdk-style packing), read exactly as
+BAMRecordReader reads a FileVirtualSplit: BGZF scan, inflate, record-boundary walk, fixed-field
++ key decode, columnar pools.  A "step" = one hbam_decode_split over the rank's split with the
+compressed bytes resident in HBM.
 
-N > 1 (torch.distributed, one rank per GPU): weak scaling — every rank decodes its own
-byte-range shard (an independent seeded 10 GB BAM), no data-path collective; the barrier
-and the max-over-ranks time are the only cross-rank operations.
+N GPUs (torch.distributed, one rank per GPU, config #4's shape): the N ranks shard ONE file of
+N x ~10 GB by byte range.  Rank r holds file bytes [off_r, off_r + S_r) (its Hadoop FileSplit)
+plus the next rank's first segment; its FileVirtualSplit is [guess(off_r), (off_r+S_r)<<16 |
+0xffff] exactly as BAMInputFormat.addProbabilisticSplits builds it, and it decodes that split
+as a window of the file (comp_base = off_r).  Nothing crosses ranks in the timed region except
+the barrier; scaling is weak (per-GPU bytes fixed).  Records of a BGZF block that starts exactly
+at a split boundary are read by both neighbouring splits, as in the reference; the record count
+check subtracts them.
 
-Prints ONE JSON line (rank 0).  roofline = k_inflate (the dominant kernel) measured with HIP
-events on the context's stream; cpu_baseline = the oracle (C restatement: zlib inflate +
-BAMRecordCodec decode + getKey) over a bounded sample on the host cores.
+Prints ONE JSON line (rank 0).  roofline = the dominant kernel (k_inflate_tokens) with HIP
+events on the context's stream, plus per-stage and whole-pipeline fractions; cpu_baseline = the
+oracle's C restatement on a bounded sample on the host cores; parity = random FileVirtualSplits
+of the benchmarked file re-read by the oracle outside the timed region.
 """
 import argparse
 import ctypes as C
@@ -30,34 +36,66 @@ import numpy as np  # noqa: E402
 
 METRIC = "uncompressed BAM GB/s + records/s decoded (whole node, 1/2/4/8 MI355X)"
 HBM_PEAK_GBS = 8000.0
+N_REF = 25  # the generator's dictionary (tools/gen_bam.cpp)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def gen_data(size, seed, threads):
+def host_threads():
+    """Threads this process may use: the box's CPU share (OMP_NUM_THREADS, 16 per GPU on the
+    pool), else every CPU."""
+    return int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def make_shard(size, seed, rank, world, threads, dist, dev):
+    """Rank's byte range of ONE file of world * m segments (+ the next rank's first segment).
+    Returns (host bytes, own length, file offset, file length, records in own range)."""
     import genbam
+    import torch
     t = time.time()
-    g = genbam.generate(target_bytes=size, seed=seed, threads=threads)
-    log("generated %.2f GB (%d records) in %.1fs" % (len(g) / 1e9, g.n_records, time.time() - t))
-    return np.asarray(g), int(g.n_records)
+    probe = genbam.generate_range(1, 0, 1, seed=seed, threads=threads)
+    m = max(1, int(round(size / len(probe))))
+    total = world * m
+    own = genbam.generate_range(total, rank * m, m, header=(rank == 0), tail=(rank == world - 1),
+                                seed=seed, threads=threads)
+    nxt = (genbam.generate_range(total, (rank + 1) * m, 1, seed=seed, threads=threads)
+           if rank < world - 1 else np.zeros(0, np.uint8))
+    sizes = [len(own)]
+    if dist:
+        st = torch.tensor([len(own)], dtype=torch.int64, device=dev)
+        allv = [torch.zeros_like(st) for _ in range(world)]
+        dist.all_gather(allv, st)
+        sizes = [int(x.item()) for x in allv]
+    off = sum(sizes[:rank])
+    buf = np.concatenate([np.asarray(own), nxt]) if len(nxt) else np.asarray(own)
+    log("rank %d: %d segments of %d, bytes [%d, %d) of a %.2f GB file, generated in %.1fs"
+        % (rank, m, total, off, off + len(own), sum(sizes) / 1e9, time.time() - t))
+    return buf, len(own), off, sum(sizes), int(own.n_records)
 
 
-def cpu_baseline(data, n_ref, first_voffset, budget_s, threads):
-    """Oracle (C restatement) on host cores: local-mode MapReduce shape — the sample is cut
-    into Hadoop FileSplits, each aligned by the oracle's BAMSplitGuesser and read by the
-    oracle's BAMRecordReader on its own thread (ctypes releases the GIL)."""
+def cpu_baseline(data, budget_s, threads):
+    """Oracle (C restatement) on host cores, local-mode MapReduce shape: a prefix of the file cut
+    into Hadoop FileSplits (one per thread), each aligned by the oracle's BAMSplitGuesser and
+    read by the oracle's BAMRecordReader on its own thread (ctypes releases the GIL)."""
     import oracle
     L = oracle.lib()
-    # bounded sample: a prefix of the file sized for ~budget_s of CPU work at ~0.2 GB/s/core
-    # uncompressed (~0.08 GB/s/core compressed)
     sample = int(min(len(data), budget_s * threads * 0.08e9))
     block = int(np.ceil(sample / threads))
     begs = list(range(0, sample, block))
     ends = [min(b + block, sample) for b in begs]
-    base = data[:sample + (1 << 20) if sample < len(data) else len(data)]
-    base = np.ascontiguousarray(base)
+    base = np.ascontiguousarray(data[:sample + (1 << 20) if sample < len(data) else len(data)])
     vs, ve = oracle.probabilistic_splits(base, np.array(begs, np.uint64), np.array(ends, np.uint64))
     counts = [0] * len(vs)
     ubytes = [0] * len(vs)
@@ -79,13 +117,66 @@ def cpu_baseline(data, n_ref, first_voffset, budget_s, threads):
     for th in ths:
         th.join()
     dt = time.time() - t
-    rec = sum(counts)
-    ub = sum(ubytes)
+    rec, ub = sum(counts), sum(ubytes)
     return {"value": round(ub / dt / 1e9, 4), "unit": "GB/s", "cores": len(vs), "kind": "port",
+            "label": "CPU restatement (oracle/hbam_oracle.c: zlib inflate + BAMRecordCodec "
+                     "decode + getKey), not the Java reference",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
             "records_per_s": round(rec / dt, 1), "seconds": round(dt, 3),
             "sample": "first %.2f GB of the same compressed file (%d records, %.2f GB uncompressed "
                       "record bytes), %d FileSplits aligned by the oracle guesser, one thread each"
                       % (sample / 1e9, rec, ub / 1e9, len(vs))}
+
+
+def parity_at_size(ctx, buf, dbuf, n_splits, seed, threads):
+    """n_splits random 32 MiB Hadoop FileSplits inside the rank's range: guess + decode on the
+    device vs guess + BAMRecordReader of the oracle, every column and every record byte."""
+    import oracle
+    rng = np.random.default_rng(seed)
+    span = len(buf) - (48 << 20)
+    if span <= 0:
+        return None
+    begs = np.sort(rng.integers(0, span, n_splits)).astype(np.int64)
+    ends = begs + (32 << 20)
+    rc, g, err = ctx.guess_batch(dbuf, begs, ends, N_REF)
+    assert rc == 0
+    sub = np.ascontiguousarray(buf)
+    mism, recs = 0, 0
+    res = [None] * n_splits
+
+    def ref_one(i):
+        go, ge = oracle.guess_bam_record_start(sub, int(begs[i]), int(ends[i]), N_REF)
+        if ge or go == int(ends[i]):
+            res[i] = (go, None)
+            return
+        r = oracle.read_split(sub, go, (int(ends[i]) << 16) | 0xffff)
+        res[i] = (go, r)
+
+    ths = [threading.Thread(target=ref_one, args=(i,)) for i in range(n_splits)]
+    for k in range(0, n_splits, threads):
+        for th in ths[k:k + threads]:
+            th.start()
+        for th in ths[k:k + threads]:
+            th.join()
+    for i in range(n_splits):
+        go, r = res[i]
+        if int(g[i]) != go:
+            mism += 1
+            continue
+        if r is None:
+            continue
+        d = ctx.decode_split(dbuf, go, (int(ends[i]) << 16) | 0xffff, n_ref=N_REF)
+        recs += r["n"]
+        same = d["rc"] == 0 and d["n"] == r["n"] and d["status"] == r["status"]
+        for k in ("voffset", "key", "block_size", "ref_id", "pos", "flag", "l_seq", "tlen"):
+            same = same and np.array_equal(d[k], r[k])
+        if same:
+            pay, _ = oracle.record_payloads(r)
+            same = d["ubuf"].tobytes() == pay.tobytes()
+        mism += 0 if same else 1
+    return {"splits": n_splits, "mismatches": mism, "records": recs,
+            "what": "random 32 MiB FileSplits of the benchmarked file: guessed start, every "
+                    "column and every record byte vs the oracle"}
 
 
 def main():
@@ -95,38 +186,43 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--size", type=float, default=10e9, help="compressed bytes per GPU")
     ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--gen-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", 16)))
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--parity-splits", type=int, default=32)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    threads = host_threads()
     import torch
     dist = None
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=dev)
 
     from hadoop_bam import _lib
     ctx = _lib.Context(local)
 
-    data, n_gen = gen_data(int(args.size), args.seed + 1000 * rank, args.gen_threads)
-    dcomp = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
-    dcomp[len(data):].zero_()
-    dcomp[:len(data)].copy_(torch.from_numpy(data), non_blocking=False)
+    buf, own_len, off, file_len, n_own = make_shard(int(args.size), args.seed, rank, world,
+                                                    threads, dist, dev)
+    dcomp = torch.empty(len(buf) + 64, dtype=torch.uint8, device=dev)
+    dcomp[len(buf):].zero_()
+    dcomp[:len(buf)].copy_(torch.from_numpy(buf), non_blocking=False)
     torch.cuda.synchronize()
-    h = ctx.parse_header(dcomp[:len(data)])
-    assert isinstance(h, dict), h
-    v_start, v_end = h["first_voffset"], (len(data) << 16) | 0xffff
-    comp_len = len(data)
+    # FileVirtualSplit of this rank's FileSplit [off, off + own_len) (BAMInputFormat.java:181-190)
+    rc, g, err = ctx.guess_batch(dcomp[:len(buf)], np.array([0], np.int64),
+                                 np.array([own_len], np.int64), N_REF)
+    if rc or err[0] or int(g[0]) == own_len:
+        raise RuntimeError("no record start in rank %d's split (rc %d err %d)" % (rank, rc, err[0]))
+    v_start = (off << 16) + int(g[0])  # the guess is relative to the window start
+    v_end = ((off + own_len) << 16) | 0xffff
 
     def step():
-        rc, cols = ctx.decode_split_device(dcomp[:comp_len], v_start, v_end, h["n_ref"])
+        rc, cols = ctx.decode_split_device(dcomp[:len(buf)], v_start, v_end, N_REF, comp_base=off,
+                                           file_len=file_len)
         if rc != 0 or cols.status != 0:
             raise RuntimeError("decode failed rc=%d status=%d: %s" % (rc, cols.status, ctx.last_error()))
         return cols
@@ -138,79 +234,121 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.time()
-    huff_ms, stage = [], None
+    huff_ms, stages = [], []
     for _ in range(args.steps):
         cols = step()
         t = ctx.timing()
         huff_ms.append(t["huffman_ms"])
-        stage = t
+        stages.append(t)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.time() - t0
-    n_rec = int(cols.n_records)
-    ubytes = int(stage["ubuf_bytes"])
-    if n_rec != n_gen:
-        raise RuntimeError("decoded %d records, generator wrote %d" % (n_rec, n_gen))
 
-    tot = torch.tensor([elapsed, float(ubytes), float(n_rec), float(comp_len)], dtype=torch.float64,
-                       device="cuda")
+    # ---- outside the timed region: record-count check, roofline inputs, parity
+    n_rec = int(cols.n_records)
+    ubytes = int(stages[-1]["ubuf_bytes"])
+    overlap = 0
+    if rank > 0 and n_rec:
+        # records of the block that starts exactly at this split's beginning: the previous split
+        # reads them too (vEnd = end<<16 | 0xffff, BAMInputFormat.java:189)
+        k = min(n_rec, 4096)
+        perm = torch.arange(k, dtype=torch.int32, device=dev)
+        head = torch.empty(k, dtype=torch.int64, device=dev)
+        assert ctx.L.hbam_permute(ctx.h, C.cast(cols.voffset, C.c_void_p), 8,
+                                  C.c_void_p(perm.data_ptr()), k, C.c_void_p(head.data_ptr())) == 0
+        overlap = int(((head.cpu() >> 16) == off).sum())
+    tot = torch.tensor([elapsed, float(ubytes), float(n_rec), float(own_len), float(n_own),
+                        float(overlap)], dtype=torch.float64, device=dev)
     if dist:
         mx = tot.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = tot.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0])
-        ub_all, rec_all, comp_all = float(sm[1]), float(sm[2]), float(sm[3])
+        ub_all, rec_all, comp_all, gen_all, ovl_all = (float(sm[i]) for i in range(1, 6))
     else:
-        ub_all, rec_all, comp_all = float(ubytes), float(n_rec), float(comp_len)
-
+        ub_all, rec_all, comp_all, gen_all, ovl_all = float(ubytes), float(n_rec), float(own_len), \
+            float(n_own), 0.0
+    if int(rec_all - ovl_all) != int(gen_all):
+        raise RuntimeError("decoded %d records (%d in boundary blocks read twice), generator wrote %d"
+                           % (rec_all, ovl_all, gen_all))
+    parity = None
+    if rank == 0 and args.parity_splits > 0:
+        try:
+            parity = parity_at_size(ctx, buf, dcomp[:len(buf)], args.parity_splits, args.seed + 17,
+                                    threads)
+        except Exception as e:  # reported, never hidden
+            parity = {"error": str(e)}
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
+
     per_step = elapsed / args.steps
     value = ub_all / per_step / 1e9
-    # dominant kernel: k_inflate_tokens (Huffman pass of the batched inflate), bracketed by HIP
-    # events on the context's stream (hbam_timing.huffman_ms).  Algorithmic bytes per launch =
-    # C read + U written (literals and match descriptors land at their final ubuf offsets),
-    # SURVEY.md §8(d) K2; k_resolve (LZ77 copies, in place) is reported in stages_ms.
+    avg = {k: float(np.mean([s[k] for s in stages])) for k in stages[0] if isinstance(stages[0][k], float)}
+    C_b, U_b, R = float(own_len), float(ubytes), float(n_rec)
+    pool_b = float(stages[-1]["pool_bytes"])
+    nblk = float(stages[-1]["n_blocks"])
+    cols_b = R * (64 + 8 + 8) + 4 * 8 * (R + 1) + pool_b  # fixed columns + key/voffset/rec_off + pools
+    # algorithmic bytes per stage; achieved = bytes / that stage's HIP-event time
+    stage_bytes = {
+        "scan": (C_b + 24 * nblk, avg["scan_ms"]),
+        "huffman": (C_b + U_b, avg["huffman_ms"]),
+        "resolve": (2 * U_b, avg["resolve_ms"]),
+        "inflate": (C_b + U_b, avg["inflate_ms"]),
+        "walk": (R * 20, avg["walk_ms"]),
+        "decode": (R * 116, avg["decode_ms"]),
+        "pools": (U_b + pool_b, avg["pools_ms"]),
+    }
+    stage_frac = {k: {"gb_s": round(b / (ms / 1e3) / 1e9, 1), "frac": round(b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "bytes": int(b), "ms": round(ms, 3)} for k, (b, ms) in stage_bytes.items() if ms > 0}
+    pipe_b = C_b + 2 * U_b + cols_b
     inf_ms = float(np.mean(huff_ms))
-    alg = comp_len + ubytes
+    alg = C_b + U_b
     achieved = alg / (inf_ms / 1e3) / 1e9
-    traffic = None
+    traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_inflate.json")
     if os.path.exists(pmc):
         try:
             pj = json.load(open(pmc))
-            if pj.get("comp_bytes") and abs(pj["comp_bytes"] - comp_len) / comp_len < 0.05 and \
-                    pj.get("kernel") == "k_inflate_tokens":
-                traffic = pj.get("hbm_bytes_per_launch")
+            if pj.get("comp_bytes") and abs(pj["comp_bytes"] - C_b) / C_b < 0.05 and \
+                    pj.get("kernel") == "k_inflate_tokens" and pj.get("tree") == "round2":
+                traffic, traffic_src = pj.get("hbm_bytes_per_launch"), "profiles/pmc_inflate.json"
         except Exception:
             traffic = None
     result = {
-        "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": args.gpus,
+        "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per_step * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (tools/gen_bam.cpp: seeded 150bp PE, zlib level 5, BGZF)",
-        "config": {"workload": "config#2: 10 GB coordinate-sorted 150bp PE BAM per GPU, BGZF "
-                               "inflate + record decode + keys + columnar pools, one "
-                               "FileVirtualSplit per GPU, input resident in HBM",
-                   "compressed_bytes_per_gpu": comp_len, "uncompressed_bytes_per_gpu": ubytes,
-                   "records_per_gpu": n_rec, "parallelism": "shard%d" % args.gpus},
+        "config": {"workload": "config#2 per GPU (config#4 shape for N>1): ~10 GB compressed "
+                               "coordinate-sorted 150bp PE BAM per GPU, one file of N x 10 GB "
+                               "sharded by byte range into guess-aligned FileVirtualSplits, BGZF "
+                               "inflate + record decode + keys + columnar pools, input resident in HBM",
+                   "compressed_bytes_per_gpu": own_len, "uncompressed_bytes_per_gpu": ubytes,
+                   "records_per_gpu": n_rec, "file_bytes": file_len,
+                   "parallelism": "shard%d" % world},
         "records_per_s": round(rec_all / per_step, 1),
-        "stages_ms": {k: round(stage[k], 3) for k in ("scan_ms", "inflate_ms", "walk_ms",
-                                                      "decode_ms", "pools_ms", "total_ms",
-                                                      "huffman_ms", "resolve_ms")},
+        "stages_ms": {k: round(avg[k], 3) for k in ("scan_ms", "inflate_ms", "huffman_ms",
+                                                    "resolve_ms", "walk_ms", "decode_ms",
+                                                    "pools_ms", "total_ms")},
         "roofline": {"bound": "hbm", "kernel": "k_inflate_tokens", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "algorithmic_bytes_per_launch": alg},
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": int(alg),
+                     "stages": stage_frac,
+                     "pipeline": {"bytes": int(pipe_b), "ms": round(avg["total_ms"], 3),
+                                  "gb_s": round(pipe_b / (avg["total_ms"] / 1e3) / 1e9, 1),
+                                  "frac": round(pipe_b / (avg["total_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                  "what": "C + 2U + columns/pools over the whole decode"}},
+        "parity": parity,
     }
     if not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(data, h["n_ref"], v_start, args.cpu_budget,
-                                                  args.gen_threads)
+            result["cpu_baseline"] = cpu_baseline(buf, args.cpu_budget, threads)
         except Exception as e:  # baseline is reported, never the target
             result["cpu_baseline"] = {"error": str(e)}
     print(json.dumps(result), flush=True)

@@ -109,6 +109,9 @@ enum BufId {
   B_S_OFF,
   B_S_HIST,
   B_S_LENS,
+  B_S_PERM,
+  B_S_RECOFF,
+  B_S_BOUNDS,
   B_COUNT_ALL
 };
 
@@ -919,8 +922,18 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
       status = s;
       err_rec = fs;
     }
-  } else if (nrec > 0 || hard_code != HBAM_EEOF) {
-    // chain ended without a stop record: the walker stopped at a CHAIN_STOP
+  } else if (hard_code == HBAM_EMORE) {
+    // The window ends exactly at a record boundary.  Withhold the last record so that the next
+    // window re-reads it together with what follows: that is where the reference's read()
+    // meets an empty BGZF block at the boundary (which ends the split).
+    n_final = nrec ? nrec - 1 : 0;
+    status = HBAM_EMORE;
+    err_rec = n_final;
+  }
+  if (status == HBAM_EMORE) {
+    // resume point for the next window: the stop record's voffset (already in voff[n_final]
+    // when that record was walked), else v_start
+    if (n_final >= nrec) HIPCHK(c, copy_sync(c, voff + n_final, &v_start, 8, hipMemcpyHostToDevice));
   }
   // ---- pools
   uint64_t tot_name = 0, tot_cig = 0, tot_seq = 0, tot_aux = 0;
@@ -987,6 +1000,172 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   return HBAM_OK;
 }
 
+// ---- streamed split read over host-resident file bytes (config #4) -------------------------
+struct hbam_split_stream {
+  hbam_ctx* c = nullptr;
+  const uint8_t* file = nullptr;
+  uint64_t file_len = 0, v_cur = 0, v_end = 0, win = 0;
+  int32_t n_ref = 0;
+  uint8_t* dbuf[2] = {nullptr, nullptr};
+  uint64_t dcap[2] = {0, 0};
+  uint64_t base[2] = {0, 0}, len[2] = {0, 0};
+  bool valid[2] = {false, false}, pending[2] = {false, false};
+  hipStream_t cs = nullptr;
+  hipEvent_t e0[2] = {nullptr, nullptr}, e1[2] = {nullptr, nullptr};
+  bool done = false;
+  uint64_t h2d_bytes = 0, windows = 0;
+  double h2d_ms = 0;
+};
+
+namespace {
+constexpr uint64_t STREAM_OVERLAP = 256 << 10;  // predicted resume point: within the last 256 KiB
+
+int stream_wait(hbam_split_stream* s, int k) {
+  if (!s->pending[k]) return HBAM_OK;
+  hbam_ctx* c = s->c;
+  HIPCHK(c, hipEventSynchronize(s->e1[k]));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, s->e0[k], s->e1[k]);
+  s->h2d_ms += ms;
+  s->h2d_bytes += s->len[k];
+  s->pending[k] = false;
+  return HBAM_OK;
+}
+
+// copy file bytes [b, b + n) into window buffer k on the copy stream (asynchronous)
+int stream_copy(hbam_split_stream* s, int k, uint64_t b, uint64_t n) {
+  hbam_ctx* c = s->c;
+  int rc = stream_wait(s, k);
+  if (rc) return rc;
+  if (s->dcap[k] < n + 64) {
+    if (s->dbuf[k]) HIPCHK(c, hipFree(s->dbuf[k]));
+    s->dbuf[k] = nullptr;
+    s->dcap[k] = 0;
+    if (hipMalloc(&s->dbuf[k], n + 64) != hipSuccess) {
+      (void)hipGetLastError();
+      return set_err(c, HBAM_ENOMEM, "hbam_split_next: hipMalloc(%llu) failed", (unsigned long long)(n + 64));
+    }
+    s->dcap[k] = n + 64;
+  }
+  HIPCHK(c, hipEventRecord(s->e0[k], s->cs));
+  if (n) HIPCHK(c, hipMemcpyAsync(s->dbuf[k], s->file + b, n, hipMemcpyHostToDevice, s->cs));
+  HIPCHK(c, hipMemsetAsync(s->dbuf[k] + n, 0, 64, s->cs));
+  HIPCHK(c, hipEventRecord(s->e1[k], s->cs));
+  s->base[k] = b;
+  s->len[k] = n;
+  s->valid[k] = true;
+  s->pending[k] = true;
+  return HBAM_OK;
+}
+}  // namespace
+
+extern "C" hbam_split_stream* hbam_split_open(hbam_ctx* c, const uint8_t* file, uint64_t file_len,
+                                         uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                                         uint64_t window_bytes) {
+  if (!c || (!file && file_len) || n_ref < 0) return nullptr;
+  if (hipSetDevice(c->device) != hipSuccess) return nullptr;
+  hbam_split_stream* s = new hbam_split_stream();
+  s->c = c;
+  s->file = file;
+  s->file_len = file_len;
+  s->v_cur = v_start;
+  s->v_end = v_end;
+  s->n_ref = n_ref;
+  s->win = std::max<uint64_t>(window_bytes, 1 << 16);
+  bool ok = hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking) == hipSuccess;
+  for (int k = 0; k < 2 && ok; ++k)
+    ok = hipEventCreate(&s->e0[k]) == hipSuccess && hipEventCreate(&s->e1[k]) == hipSuccess;
+  if (!ok) {
+    (void)hipGetLastError();
+    hbam_split_close(s);
+    return nullptr;
+  }
+  return s;
+}
+
+extern "C" int hbam_split_next(hbam_split_stream* s, hbam_columns* out) {
+  if (!s || !out) return HBAM_EINVAL;
+  hbam_ctx* c = s->c;
+  memset(out, 0, sizeof *out);
+  if (s->done) return 0;
+  HIPCHK(c, hipSetDevice(c->device));
+  for (;;) {
+    const uint64_t ws = std::min(s->v_cur >> 16, s->file_len);
+    const uint64_t ahead = std::min<uint64_t>(s->win / 2, s->file_len - ws);
+    int k = -1;
+    for (int b = 0; b < 2; ++b)
+      if (s->valid[b] && s->base[b] <= ws && s->base[b] + s->len[b] >= ws + ahead &&
+          (ws < s->base[b] + s->len[b] || s->base[b] + s->len[b] == s->file_len))
+        k = b;
+    if (k < 0) {  // not predicted (first window, long record, grown window): copy it now
+      k = s->valid[0] && !s->valid[1] ? 1 : 0;
+      int rc = stream_copy(s, k, ws, std::min(s->win, s->file_len - ws));
+      if (rc) return rc;
+    }
+    int rc = stream_wait(s, k);
+    if (rc) return rc;
+    // prefetch the predicted next window into the other buffer while this one decodes
+    const uint64_t wend = s->base[k] + s->len[k];
+    const int o = 1 - k;
+    if (wend < s->file_len) {
+      const uint64_t ov = std::min<uint64_t>(STREAM_OVERLAP, s->win / 2);
+      const uint64_t ps = std::max(s->base[k], wend > ov ? wend - ov : 0);
+      if (!(s->valid[o] && s->base[o] == ps))
+        if ((rc = stream_copy(s, o, ps, std::min(s->win, s->file_len - ps)))) return rc;
+    }
+    ++s->windows;
+    const uint8_t* w = s->dbuf[k] ? s->dbuf[k] : (const uint8_t*)s->dbuf[o];
+    if (!w) {  // empty file: nothing was ever allocated
+      if ((rc = stream_copy(s, k, ws, 0)) || (rc = stream_wait(s, k))) return rc;
+      w = s->dbuf[k];
+    }
+    rc = hbam_decode_split(c, w, 1, s->base[k], s->len[k], s->file_len, s->v_cur, s->v_end, s->n_ref, out);
+    if (rc) return rc;
+    if (out->status != HBAM_EMORE) {
+      s->done = true;
+      return 1;
+    }
+    uint64_t resume = s->v_cur;
+    if (out->voffset) HIPCHK(c, copy_sync(c, &resume, out->voffset + out->n_records, 8, hipMemcpyDeviceToHost));
+    out->status = HBAM_OK;
+    out->err_record = 0;
+    if (resume == s->v_cur && out->n_records == 0) {
+      // not one record fits: a longer window, copied at the resume point
+      if (wend >= s->file_len)
+        return set_err(c, HBAM_EINVAL, "hbam_split_next: no progress at voffset %llu", (unsigned long long)s->v_cur);
+      for (int b = 0; b < 2; ++b) {
+        if ((rc = stream_wait(s, b))) return rc;
+        s->valid[b] = false;
+      }
+      s->win *= 2;
+      continue;
+    }
+    s->v_cur = resume;
+    if (out->n_records) return 1;
+  }
+}
+
+extern "C" int hbam_split_stats(const hbam_split_stream* s, uint64_t* h2d_bytes, double* h2d_ms, uint64_t* windows) {
+  if (!s) return HBAM_EINVAL;
+  if (h2d_bytes) *h2d_bytes = s->h2d_bytes;
+  if (h2d_ms) *h2d_ms = s->h2d_ms;
+  if (windows) *windows = s->windows;
+  return HBAM_OK;
+}
+
+extern "C" void hbam_split_close(hbam_split_stream* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->c->device);
+  if (s->cs) (void)hipStreamSynchronize(s->cs);
+  for (int k = 0; k < 2; ++k) {
+    if (s->dbuf[k]) (void)hipFree(s->dbuf[k]);
+    if (s->e0[k]) (void)hipEventDestroy(s->e0[k]);
+    if (s->e1[k]) (void)hipEventDestroy(s->e1[k]);
+  }
+  if (s->cs) (void)hipStreamDestroy(s->cs);
+  delete s;
+}
+
 extern "C" int hbam_columns_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_columns* h) {
   if (!c || !dv || !h) return HBAM_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));
@@ -1035,9 +1214,21 @@ extern "C" int hbam_columns_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_co
   ALLOC(seq, uint8_t, ns)
   ALLOC(qual, uint8_t, ns)
   ALLOC(aux, uint8_t, na)
+  // the records' bytes (SAMRecordWritable payloads: block_size + record), rec_off rebased to them
+  uint64_t lo = 0, hi = 0;
+  if (n) {
+    lo = h->rec_off[0];
+    hi = h->rec_off[n - 1] + 4 + (uint64_t)(uint32_t)h->block_size[n - 1];
+    if (hi < lo || hi > dv->ubuf_len + UBUF_SLACK)
+      return set_err(c, HBAM_EINVAL, "hbam_columns_to_host: record bytes outside ubuf");
+  }
+  h->ubuf = (uint8_t*)malloc(hi > lo ? hi - lo : 1);
+  if (!h->ubuf) return HBAM_ENOMEM;
+  if ((rc = cp(h->ubuf, dv->ubuf + lo, hi - lo))) return rc;
 #undef ALLOC
-  h->ubuf = nullptr;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint64_t i = 0; i < n; ++i) h->rec_off[i] -= lo;
+  h->ubuf_len = hi - lo;
   return HBAM_OK;
 }
 
@@ -1046,7 +1237,7 @@ extern "C" void hbam_free_host_columns(hbam_columns* h) {
   void* ps[] = {h->voffset, h->key, h->rec_off, h->block_size, h->ref_id, h->pos, h->l_read_name,
                 h->mapq, h->bin, h->n_cigar, h->flag, h->l_seq, h->next_ref_id, h->next_pos, h->tlen,
                 h->layout_ok, h->name_off, h->cigar_off, h->seq_off, h->aux_off, h->names, h->cigars,
-                h->seq, h->qual, h->aux};
+                h->seq, h->qual, h->aux, h->ubuf};
   for (void* p : ps) free(p);
   memset(h, 0, sizeof *h);
 }
@@ -1373,6 +1564,100 @@ extern "C" int hbam_permute(hbam_ctx* c, const void* src, uint32_t elem_size, co
   }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return HBAM_OK;
+}
+
+extern "C" int hbam_device_alloc(hbam_ctx* c, uint64_t bytes, void** dev_out) {
+  if (!c || !dev_out) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  void* d = nullptr;
+  if (hipMalloc(&d, bytes ? bytes : 1) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(c, HBAM_ENOMEM, "hbam_device_alloc(%llu) failed", (unsigned long long)bytes);
+  }
+  *dev_out = d;
+  return HBAM_OK;
+}
+
+namespace {
+// sorted run of n records whose bytes sit at ubuf[rec_off[i]] (block_size[i] + 4 bytes each)
+int sort_run(hbam_ctx* c, const int64_t* key, const uint64_t* voffset, const int32_t* block_size,
+             const uint8_t* ubuf, const uint64_t* rec_off, uint64_t n, hbam_sorted_run* out) {
+  int rc;
+  uint64_t total = 0;
+  if (!out->payload) {  // size query
+    uint64_t* off;
+    if ((rc = ensure(c, B_S_OFF, n + 1, &off))) return rc;
+    if ((rc = hbam_gather_records(c, ubuf, rec_off, block_size, nullptr, n, nullptr, 0, off, &total)))
+      return rc;
+    out->n = n;
+    out->payload_bytes = total;
+    return HBAM_OK;
+  }
+  if (n && (!out->key || !out->voffset || !out->block_size || !out->offsets)) return HBAM_EINVAL;
+  uint32_t* perm;
+  if ((rc = ensure(c, B_S_PERM, n + 1, &perm))) return rc;
+  if ((rc = hbam_sort_keys(c, key, n, out->key, perm))) return rc;
+  if ((rc = hbam_permute(c, voffset, 8, perm, n, out->voffset))) return rc;
+  if ((rc = hbam_permute(c, block_size, 4, perm, n, out->block_size))) return rc;
+  if ((rc = hbam_gather_records(c, ubuf, rec_off, block_size, perm, n, out->payload,
+                                out->payload_bytes, out->offsets, &total)))
+    return rc;
+  out->n = n;
+  out->payload_bytes = total;
+  return HBAM_OK;
+}
+}  // namespace
+
+extern "C" int hbam_sort_split(hbam_ctx* c, const hbam_columns* dv, hbam_sorted_run* out) {
+  if (!c || !dv || !out) return HBAM_EINVAL;
+  if (dv->status != HBAM_OK) return set_err(c, dv->status, "hbam_sort_split: the decode raised %d", dv->status);
+  HIPCHK(c, hipSetDevice(c->device));
+  return sort_run(c, dv->key, dv->voffset, dv->block_size, dv->ubuf, dv->rec_off, dv->n_records, out);
+}
+
+extern "C" int hbam_sort_received(hbam_ctx* c, const int64_t* key, const int64_t* voffset,
+                                  const int32_t* block_size, const uint8_t* payload, uint64_t n,
+                                  hbam_sorted_run* out) {
+  if (!c || !out || (n && (!key || !voffset || !block_size || !payload))) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  // record offsets of the received payload: exclusive scan of 4 + block_size
+  uint64_t* rec_off;
+  int rc;
+  if ((rc = ensure(c, B_S_RECOFF, n + 1, &rec_off))) return rc;
+  uint64_t total = 0;
+  if ((rc = hbam_gather_records(c, nullptr, nullptr, block_size, nullptr, n, nullptr, 0, rec_off, &total)))
+    return rc;
+  return sort_run(c, key, (const uint64_t*)voffset, block_size, payload, rec_off, n, out);
+}
+
+extern "C" int hbam_sort_partition(hbam_ctx* c, const hbam_sorted_run* run, const int64_t* split_points,
+                                   uint32_t nparts, uint64_t* rec_bounds, uint64_t* byte_bounds) {
+  if (!c || !run || !rec_bounds || !byte_bounds || nparts == 0 || (nparts > 1 && !split_points))
+    return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint32_t m = nparts - 1;
+  rec_bounds[0] = 0;
+  byte_bounds[0] = 0;
+  rec_bounds[nparts] = run->n;
+  byte_bounds[nparts] = run->payload_bytes;
+  if (m == 0) return HBAM_OK;
+  if (run->n && (!run->key || !run->offsets)) return HBAM_EINVAL;
+  uint64_t* d;
+  int rc;
+  if ((rc = ensure(c, B_S_BOUNDS, 3 * (uint64_t)m, &d))) return rc;
+  int64_t* dsp = (int64_t*)(d + 2 * (uint64_t)m);
+  HIPCHK(c, hipMemcpyAsync(dsp, split_points, 8ull * m, hipMemcpyHostToDevice, c->stream));
+  if (run->n) {
+    k_sort_bounds<<<grid_for(m, RS_WG), RS_WG, 0, c->stream>>>(run->key, run->n, dsp, m, run->offsets, d,
+                                                               d + m);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(rec_bounds + 1, d, 8ull * m, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(byte_bounds + 1, d + m, 8ull * m, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  } else {
+    for (uint32_t j = 1; j < nparts; ++j) rec_bounds[j] = byte_bounds[j] = 0;
+  }
   return HBAM_OK;
 }
 

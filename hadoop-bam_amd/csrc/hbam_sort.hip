@@ -167,6 +167,26 @@ __global__ __launch_bounds__(RS_WG) void k_gather_records(const uint8_t* __restr
   }
 }
 
+// TotalOrderPartitioner bounds: for split point j, the first index whose (signed) key is
+// greater (partition j holds keys <= sp[j]); sorted keys, one thread per split point
+__global__ __launch_bounds__(RS_WG) void k_sort_bounds(const int64_t* __restrict__ keys, uint64_t n,
+                                                       const int64_t* __restrict__ sp, uint32_t m,
+                                                       const uint64_t* __restrict__ offsets,
+                                                       uint64_t* __restrict__ rec_b,
+                                                       uint64_t* __restrict__ byte_b) {
+  const uint32_t j = blockIdx.x * RS_WG + threadIdx.x;
+  if (j >= m) return;
+  const int64_t v = sp[j];
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (keys[mid] <= v) lo = mid + 1;
+    else hi = mid;
+  }
+  rec_b[j] = lo;
+  byte_b[j] = offsets[lo];
+}
+
 // SplittingBAMIndexer (SplittingBAMIndexer.java:146-248): the voffset before every
 // granularity-th record (records counted from 1) of a whole-file decode
 __global__ __launch_bounds__(RS_WG) void k_index_pick(const uint64_t* __restrict__ voffset, uint64_t n,

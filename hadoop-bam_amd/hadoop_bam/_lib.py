@@ -44,7 +44,9 @@ EXPORTS = [
     "hbam_release_columns", "hbam_guess_bam_record_start", "hbam_guess_batch",
     "hbam_guess_bgzf_block_start", "hbam_probabilistic_splits",
     "hbam_sort_keys", "hbam_gather_records", "hbam_permute", "hbam_splitting_index",
-    "hbam_bgzf_block_index", "hbam_resolve_tokens",
+    "hbam_bgzf_block_index", "hbam_resolve_tokens", "hbam_split_open", "hbam_split_next",
+    "hbam_split_stats", "hbam_split_close", "hbam_device_alloc", "hbam_sort_split",
+    "hbam_sort_partition", "hbam_sort_received",
 ]
 
 
@@ -73,6 +75,12 @@ class Timing(C.Structure):
                                           "huffman_ms", "resolve_ms")] + \
                [(n, C.c_uint64) for n in ("n_blocks", "comp_bytes", "ubuf_bytes", "n_records",
                                           "pool_bytes", "reserved")]
+
+
+class SortedRunC(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("payload_bytes", C.c_uint64), ("key", C.c_void_p),
+                ("voffset", C.c_void_p), ("block_size", C.c_void_p), ("offsets", C.c_void_p),
+                ("payload", C.c_void_p)]
 
 
 _u8p = C.POINTER(C.c_uint8)
@@ -151,6 +159,15 @@ def load(path=None):
         "hbam_bgzf_block_index": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_int32, vp,
                                               C.c_uint64]),
         "hbam_resolve_tokens": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, C.c_uint32, _i32p]),
+        "hbam_split_open": (vp, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64]),
+        "hbam_split_next": (C.c_int, [vp, C.POINTER(Columns)]),
+        "hbam_split_stats": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_double),
+                                       C.POINTER(C.c_uint64)]),
+        "hbam_split_close": (None, [vp]),
+        "hbam_device_alloc": (C.c_int, [vp, C.c_uint64, C.POINTER(vp)]),
+        "hbam_sort_split": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(SortedRunC)]),
+        "hbam_sort_partition": (C.c_int, [vp, C.POINTER(SortedRunC), vp, C.c_uint32, vp, vp]),
+        "hbam_sort_received": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, C.POINTER(SortedRunC)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -170,6 +187,8 @@ def host_columns_to_numpy(h):
     for name in ("name_off", "cigar_off", "seq_off", "aux_off"):
         p = getattr(h, name)
         out[name] = np.ctypeslib.as_array(p, shape=(n + 1,)).copy() if p else np.zeros(1, np.uint64)
+    ul = int(h.ubuf_len)
+    out["ubuf"] = np.ctypeslib.as_array(h.ubuf, shape=(ul,)).copy() if (ul and h.ubuf) else np.zeros(0, np.uint8)
     pools = [("names", np.uint8, "name_off"), ("cigars", np.uint32, "cigar_off"),
              ("seq", np.uint8, "seq_off"), ("qual", np.uint8, "seq_off"),
              ("aux", np.uint8, "aux_off")]
@@ -291,6 +310,41 @@ class Context:
         out["rc"] = 0
         out["timing"] = self.timing()
         return out
+
+    def split_stream(self, data, v_start, v_end, n_ref, window_bytes=1 << 30):
+        """Streamed BAMRecordReader over a host-resident file (hbam_split_open/next): yields
+        the host columns of each window in order; the last one carries the split's status."""
+        a = np.ascontiguousarray(np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray)
+                                 else data, dtype=np.uint8)
+        keep = a if a.size else np.zeros(1, np.uint8)
+        s = self.L.hbam_split_open(self.h, C.c_void_p(keep.ctypes.data), a.size, v_start, v_end,
+                                   int(n_ref), int(window_bytes))
+        if not s:
+            raise HbamUnavailable("hbam_split_open failed: %s" % self.last_error())
+        try:
+            while True:
+                d = Columns()
+                rc = self.L.hbam_split_next(s, C.byref(d))
+                if rc < 0:
+                    raise RuntimeError("hbam_split_next failed (%d): %s" % (rc, self.last_error()))
+                if rc == 0:
+                    return
+                h = Columns()
+                rc = self.L.hbam_columns_to_host(self.h, C.byref(d), C.byref(h))
+                if rc:
+                    raise RuntimeError("hbam_columns_to_host failed (%d): %s" % (rc, self.last_error()))
+                out = host_columns_to_numpy(h)
+                self.L.hbam_free_host_columns(C.byref(h))
+                yield out
+        finally:
+            self.last_stream_stats = self._split_stats(s)
+            self.L.hbam_split_close(s)
+
+    def _split_stats(self, s):
+        b, w = C.c_uint64(0), C.c_uint64(0)
+        ms = C.c_double(0)
+        self.L.hbam_split_stats(s, C.byref(b), C.byref(ms), C.byref(w))
+        return {"h2d_bytes": int(b.value), "h2d_ms": float(ms.value), "windows": int(w.value)}
 
     def decode_split_device(self, data, v_start, v_end, n_ref, comp_base=0, file_len=None):
         """Device-resident decode (bench path): returns the hbam_columns struct."""

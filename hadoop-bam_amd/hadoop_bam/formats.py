@@ -491,6 +491,9 @@ class BAMRecordView:
         a, b = int(c["seq_off"][self._i]), int(c["seq_off"][self._i + 1])
         return bytes(c["qual"][a:b])
 
+    def getReadBases(self):
+        return self.getReadString().encode() if self.getReadString() != "*" else b""
+
     def getVariableBinaryRepresentation(self):
         return self._dec.var_block(self._i)
 
@@ -514,21 +517,84 @@ class SAMRecordWritable:
     def write(self, out):
         out.write(self.record.toBAMBytes())
 
-    def readFields(self, inp):
+    def readFields(self, inp):  # :66-69, lazy decode (LazyBAMRecordFactory)
         bs = struct.unpack("<i", inp.read(4))[0]
         body = inp.read(bs)
-        self.record = _StandaloneRecord(struct.pack("<i", bs) + body)
+        self.record = BAMRecordBytes(struct.pack("<i", bs) + body)
 
 
-class _StandaloneRecord:
+class BAMRecordBytes:
+    """A lazily decoded BAM record over its wire bytes (block_size + record), as
+    SAMRecordWritable.readFields builds it with LazyBAMRecordFactory (LazyBAMRecordFactory.java
+    :31-99): fixed fields are read on access, the variable block is kept verbatim."""
+
     def __init__(self, raw):
-        self.raw = raw
+        self.raw = bytes(raw)
+        (self._bs, self._ref, self._pos, self._lrn, self._mapq, self._bin, self._ncig, self._flag,
+         self._lseq, self._nref, self._npos, self._tlen) = struct.unpack_from("<iiiBBHHHiiii", self.raw, 0)
 
     def toBAMBytes(self):
         return self.raw
 
     def getVariableBinaryRepresentation(self):
         return self.raw[36:]
+
+    def getReferenceIndex(self):
+        return self._ref
+
+    def getAlignmentStart(self):
+        return _i32(self._pos + 1)
+
+    def getFlags(self):
+        return self._flag
+
+    def getReadUnmappedFlag(self):
+        return bool(self._flag & 4)
+
+    def getMappingQuality(self):
+        return self._mapq
+
+    def getMateReferenceIndex(self):
+        return self._nref
+
+    def getMateAlignmentStart(self):
+        return _i32(self._npos + 1)
+
+    def getInferredInsertSize(self):
+        return self._tlen
+
+    def getIndexingBin(self):
+        return self._bin
+
+    def _var(self):
+        v = self.raw[36:]
+        p = self._lrn
+        cig = v[p:p + 4 * self._ncig]
+        p += 4 * self._ncig
+        seq = v[p:p + (self._lseq + 1) // 2]
+        p += (self._lseq + 1) // 2
+        return v, cig, seq, v[p:p + self._lseq]
+
+    def getReadName(self):
+        return self.raw[36:36 + max(self._lrn - 1, 0)].decode("latin-1")
+
+    def getCigarString(self):
+        _, cig, _, _ = self._var()
+        ops = struct.unpack("<%dI" % (len(cig) // 4), cig)
+        return "".join("%d%s" % (o >> 4, "MIDNSHP=X"[o & 15]) for o in ops) or "*"
+
+    def getReadString(self):
+        _, _, seq, _ = self._var()
+        a = "=ACMGRSVTWYHKDBN"
+        out = "".join(a[b >> 4] + a[b & 15] for b in seq)[:self._lseq]
+        return out or "*"
+
+    def getReadBases(self):
+        s = self.getReadString()
+        return s.encode() if s != "*" else b""
+
+    def getBaseQualities(self):
+        return self._var()[3]
 
 
 class LongWritable:
@@ -543,32 +609,147 @@ class LongWritable:
 
 
 # ---- the record reader ---------------------------------------------------------------
-class _DecodedSplit:
-    def __init__(self, cols, ubuf_host=None):
-        self.cols = cols
-        self.ubuf = ubuf_host
+_M64 = (1 << 64) - 1
+_C1, _C2 = 0x87c37b91114253d5, 0x4cf5ad432745937f
 
-    def var_block(self, i):
-        c = self.cols
-        if self.ubuf is not None:
-            r = int(c["rec_off"][i])
-            return bytes(self.ubuf[r + 36:r + 4 + int(c["block_size"][i])])
-        raise NotImplementedError("raw payload not downloaded")
+
+def _rotl(x, r):
+    return ((x << r) | (x >> (64 - r))) & _M64
+
+
+def _fmix(k):
+    k ^= k >> 33
+    k = (k * 0xff51afd7ed558ccd) & _M64
+    k ^= k >> 33
+    k = (k * 0xc4ceb9fe1a85ec53) & _M64
+    return k ^ (k >> 33)
+
+
+def _s64(x):
+    return x - (1 << 64) if x >> 63 else x
+
+
+def _finish(h1, h2, n):
+    h1 ^= n & _M64
+    h2 ^= n & _M64
+    h1 = (h1 + h2) & _M64
+    h2 = (h2 + h1) & _M64
+    h1, h2 = _fmix(h1), _fmix(h2)
+    return _s64((h1 + h2) & _M64)
+
+
+def _mix_block(h1, h2, k1, k2):
+    k1 = (k1 * _C1) & _M64
+    k1 = (_rotl(k1, 31) * _C2) & _M64
+    h1 ^= k1
+    h1 = (_rotl(h1, 27) + h2) & _M64
+    h1 = (h1 * 5 + 0x52dce729) & _M64
+    k2 = (k2 * _C2) & _M64
+    k2 = (_rotl(k2, 33) * _C1) & _M64
+    h2 ^= k2
+    h2 = ((h2 << 31) | (h1 >> 33)) & _M64  # MurmurHash3.java:59 mixes h1 in here
+    h2 = (h2 + h1) & _M64
+    h2 = (h2 * 5 + 0x38495ab5) & _M64
+    return h1, h2
+
+
+def murmurhash3_bytes(key, seed=0):
+    """util/MurmurHash3.java:32-102 (byte[] variant, incl. the line-59 h2 quirk)."""
+    key = bytes(key)
+    n = len(key)
+    h1 = h2 = seed & _M64
+    nb = n // 16
+    for i in range(nb):
+        k1, k2 = struct.unpack_from("<QQ", key, 16 * i)
+        h1, h2 = _mix_block(h1, h2, k1, k2)
+    t = key[16 * nb:]
+    k1 = k2 = 0
+    if len(t) > 8:
+        for j in range(len(t) - 1, 7, -1):
+            k2 ^= t[j] << (8 * (j - 8))
+        k2 = (_rotl((k2 * _C2) & _M64, 33) * _C1) & _M64
+        h2 ^= k2
+    if len(t):
+        for j in range(min(len(t), 8) - 1, -1, -1):
+            k1 ^= t[j] << (8 * j)
+        k1 = (_rotl((k1 * _C1) & _M64, 31) * _C2) & _M64
+        h1 ^= k1
+    return _finish(h1, h2, n)
+
+
+def murmurhash3_chars(chars, seed=0):
+    """util/MurmurHash3.java:108-171 (CharSequence variant: UTF-16 code units; the tail reads
+    charAt(0..6) from the START of the sequence, as the reference does)."""
+    c = [ord(x) for x in str(chars)]
+    n = len(c)
+    h1 = h2 = seed & _M64
+    for i in range(n // 8):
+        i0, i1 = 8 * i, 8 * i + 4
+        k1 = c[i0] | c[i0 + 1] << 16 | c[i0 + 2] << 32 | c[i0 + 3] << 48
+        k2 = c[i1] | c[i1 + 1] << 16 | c[i1 + 2] << 32 | c[i1 + 3] << 48
+        h1, h2 = _mix_block(h1, h2, k1, k2)
+    r = n & 7
+    k1 = k2 = 0
+    if r >= 5:
+        for j in range(r - 1, 3, -1):
+            k2 ^= c[j] << (16 * (j - 4))
+        k2 = (_rotl((k2 * _C2) & _M64, 33) * _C1) & _M64
+        h2 ^= k2
+    if r >= 1:
+        for j in range(min(r, 4) - 1, -1, -1):
+            k1 ^= c[j] << (16 * j)
+        k1 = (_rotl((k1 * _C1) & _M64, 31) * _C2) & _M64
+        h1 ^= k1
+    return _finish(h1, h2, n)
+
+
+def _i32(x):
+    x &= 0xffffffff
+    return x - (1 << 32) if x >> 31 else x
+
+
+class _DecodedSplit:
+    """One window's host columns; ubuf holds exactly the records' bytes (rec_off into it)."""
+
+    def __init__(self, cols):
+        self.cols = cols
+        self.ubuf = cols.get("ubuf")
 
     def record_bytes(self, i):
         r = int(self.cols["rec_off"][i])
         return bytes(self.ubuf[r:r + 4 + int(self.cols["block_size"][i])])
 
+    def var_block(self, i):
+        r = int(self.cols["rec_off"][i])
+        return bytes(self.ubuf[r + 36:r + 4 + int(self.cols["block_size"][i])])
+
+
+WINDOW_BYTES_PROPERTY = "hadoopbam.hip.window-bytes"
+
+
+def read_header(data, ctx):
+    """SAMHeaderReader.readSAMHeaderFrom (util/SAMHeaderReader.java:53-72) on the device, from a
+    growing prefix of the file (the header is usually one or two BGZF blocks)."""
+    n = min(len(data), 1 << 20)
+    while True:
+        h = ctx.parse_header(data[:n])
+        if isinstance(h, dict) or n >= len(data):
+            return h
+        n = min(len(data), 4 * n)
+
 
 class BAMRecordReader:
-    """BAMRecordReader.java:48-188.  initialize() decodes the whole split on the GPU;
-    nextKeyValue() walks the columns and raises the reference's exception at the record
-    where the reference would raise it."""
+    """BAMRecordReader.java:48-188.  initialize() opens a streamed device decode of the split
+    (hbam_split_open: windows of hadoopbam.hip.window-bytes compressed bytes, the next one
+    copied while the current one decodes); nextKeyValue() walks each window's columns and
+    raises the reference's exception at the record where the reference raises it.  The key
+    and value objects are reused, as in the reference (:53-54, :185-186)."""
 
     def __init__(self):
         self.key = LongWritable()
         self.record = SAMRecordWritable()
         self._init = False
+        self._gen = None
 
     @staticmethod
     def getKey0(ref_idx, alignment_start0):
@@ -577,10 +758,23 @@ class BAMRecordReader:
         return ((v + (1 << 63)) % (1 << 64)) - (1 << 63)
 
     @staticmethod
-    def getKey(ref_idx_or_record, alignment_start=None):
+    def getKey(rec, alignment_start=None):
+        """getKey(SAMRecord) (:66-96) or getKey(int refIdx, int alignmentStart) (:99-101)."""
         if alignment_start is not None:
-            return BAMRecordReader.getKey0(ref_idx_or_record, alignment_start - 1)
-        raise NotImplementedError("getKey(SAMRecord) is computed on the device (key column)")
+            return BAMRecordReader.getKey0(rec, _i32(int(alignment_start) - 1))
+        ref_idx = int(rec.getReferenceIndex())
+        start = int(rec.getAlignmentStart())
+        if not (rec.getReadUnmappedFlag() or ref_idx < 0 or start < 0):
+            return BAMRecordReader.getKey0(ref_idx, _i32(start - 1))
+        var = rec.getVariableBinaryRepresentation()
+        if var is not None:  # undecoded BAM record: hash its raw variable block
+            h = _i32(murmurhash3_bytes(var, 0))
+        else:  # decoded record: a few representative fields, chained (:88-93)
+            h = _i32(murmurhash3_chars(rec.getReadName(), 0))
+            h = _i32(murmurhash3_bytes(rec.getReadBases(), h))
+            h = _i32(murmurhash3_bytes(rec.getBaseQualities(), h))
+            h = _i32(murmurhash3_chars(rec.getCigarString(), h))
+        return BAMRecordReader.getKey0(0x7fffffff, h)
 
     def initialize(self, split, ctx=None):
         if self._init:
@@ -588,43 +782,50 @@ class BAMRecordReader:
         self._init = True
         conf = ctx if isinstance(ctx, Configuration) else Configuration()
         self.split = split
-        data = _read_file(split.getPath())
-        self.ctxt = context(conf)
-        cols = self.ctxt.decode_split(data, split.getStartVirtualOffset(),
-                                      split.getEndVirtualOffset(), n_ref=-1)
-        if cols["rc"]:
-            raise_for(cols["rc"], cols.get("error", ""))
-        if cols["n"] == 0 and cols["status"] != 0:
-            raise_for(cols["status"], "BAMRecordReader.initialize")
-        self.dec = _DecodedSplit(cols, None)
-        self._ubuf = None
+        path = split.getPath()
+        data = path if isinstance(path, (bytes, bytearray, np.ndarray)) else np.memmap(path, np.uint8, "r")
         self._data = data
-        self.i = 0
-        self.n = cols["n"]
-        self.status = cols["status"]
+        self.ctxt = context(conf)
+        h = read_header(data, self.ctxt)
+        if isinstance(h, int):
+            raise_for(h, "cannot read SAM header")
+        window = int(conf.get(WINDOW_BYTES_PROPERTY, 1 << 30))
+        self._gen = self.ctxt.split_stream(data, split.getStartVirtualOffset(),
+                                           split.getEndVirtualOffset(), h["n_ref"], window)
+        self.dec = None
+        self.i = self.n = 0
+        self.status = 0
+        self._last = False
         self.file_start = split.getStartVirtualOffset() >> 16
         self.v_end = split.getEndVirtualOffset()
+        self._next_window()
 
-    def _payload(self):
-        if self.dec.ubuf is None:
-            # inflated stream for SAMRecordWritable payloads (lazy: only if records are read)
-            rc, blocks = self.ctxt.scan_blocks(self._data)
-            rc2, u, off, st = self.ctxt.inflate(self._data, blocks, check_crc=False)
-            start_blk = int(np.searchsorted(blocks["coff"], self.split.getStartVirtualOffset() >> 16))
-            base = int(off[start_blk])
-            self.dec.ubuf = np.asarray(u[base:])
-        return self.dec
+    def _next_window(self):
+        try:
+            cols = next(self._gen)
+        except StopIteration:
+            self._last = True
+            self.dec, self.i, self.n, self.status = None, 0, 0, 0
+            return False
+        self.dec = _DecodedSplit(cols)
+        self.i, self.n, self.status = 0, cols["n"], cols["status"]
+        if self.status != 0:
+            self._last = True
+        return True
 
     def nextKeyValue(self):
-        if self.i >= self.n:
-            if self.status != 0 and self.i == self.n:
-                self.i += 1
-                raise_for(self.status, "at record %d" % self.n)
+        while self.dec is not None and self.i >= self.n:
+            if self.status != 0:
+                st, self.status = self.status, 0
+                raise_for(st, "at record %d of the window" % self.n)
+            if self._last or not self._next_window():
+                return False
+        if self.dec is None:
             return False
         i = self.i
         self.i += 1
         self.key.set(int(self.dec.cols["key"][i]))
-        self.record.set(BAMRecordView(self._payload(), i))
+        self.record.set(BAMRecordView(self.dec, i))
         return True
 
     def getCurrentKey(self):
@@ -633,14 +834,17 @@ class BAMRecordReader:
     def getCurrentValue(self):
         return self.record
 
-    def getProgress(self):
-        if self.i >= self.n:
-            return 1.0
+    def getProgress(self):  # :157-168
+        if self.dec is None or self.i >= self.n:
+            return 1.0 if self._last else 0.0
         vp = int(self.dec.cols["voffset"][self.i])
         file_end = self.v_end >> 16
         return float((vp >> 16) - self.file_start) / (file_end - self.file_start + 1)
 
     def close(self):
+        if self._gen is not None:
+            self._gen.close()
+        self._gen = None
         self.dec = None
 
 

@@ -85,45 +85,53 @@ class HipSortOps:
                                       n, C.c_void_p(out.data_ptr())), "hbam_permute")
         return out
 
-    def _gather(self, ubuf_ptr, rec_off_ptr, bs_ptr, perm_ptr, n, size_only=False):
+    def _run(self, call, n_hint):
+        """Size query, torch-owned outputs, then the call itself (hbam_sort_split/received)."""
+        from ._lib import SortedRunC
         t = self.torch
+        q = SortedRunC()
+        self._chk(call(C.byref(q)), "sorted-run size query")
+        n, nb = int(q.n), int(q.payload_bytes)
+        keys = t.empty(max(n, 1), dtype=t.int64, device=self.dev)
+        vo = t.empty(max(n, 1), dtype=t.int64, device=self.dev)
+        bs = t.empty(max(n, 1), dtype=t.int32, device=self.dev)
         off = t.empty(n + 1, dtype=t.int64, device=self.dev)
+        pay = t.empty(max(nb, 1), dtype=t.uint8, device=self.dev)
+        r = SortedRunC(n, nb, keys.data_ptr(), vo.data_ptr(), bs.data_ptr(), off.data_ptr(),
+                       pay.data_ptr())
         self._after_torch()
-        tot = C.c_uint64(0)
-        self._chk(self.L.hbam_gather_records(self.ctx.h, C.c_void_p(ubuf_ptr), C.c_void_p(rec_off_ptr),
-                                             C.c_void_p(bs_ptr), C.c_void_p(perm_ptr), n, None, 0,
-                                             C.c_void_p(off.data_ptr()), C.byref(tot)),
-                  "hbam_gather_records(size)")
-        if size_only:
-            return None, off
-        out = t.empty(max(int(tot.value), 1), dtype=t.uint8, device=self.dev)
-        self._chk(self.L.hbam_gather_records(self.ctx.h, C.c_void_p(ubuf_ptr), C.c_void_p(rec_off_ptr),
-                                             C.c_void_p(bs_ptr), C.c_void_p(perm_ptr), n,
-                                             C.c_void_p(out.data_ptr()), out.numel(),
-                                             C.c_void_p(off.data_ptr()), C.byref(tot)),
-                  "hbam_gather_records")
-        return out[:int(tot.value)], off
+        self._chk(call(C.byref(r)), "sorted run")
+        if n == 0:
+            off.zero_()
+        return SortedRun(keys[:n], vo[:n], bs[:n], pay[:nb], off)
 
     def run_from_columns(self, cols):
-        """Sorted run of a decoded split (device hbam_columns from decode_split_device)."""
-        n = int(cols.n_records)
-        keys, perm = self._sort(_addr(cols.key), n)
-        vo = self._permute(_addr(cols.voffset), 8, perm, n)
-        bs = self._permute(_addr(cols.block_size), 4, perm, n)
-        payload, off = self._gather(_addr(cols.ubuf), _addr(cols.rec_off), _addr(cols.block_size),
-                                    perm.data_ptr(), n)
-        return SortedRun(keys, vo, bs, payload, off)
+        """hbam_sort_split: sorted run of a decoded split (device hbam_columns)."""
+        return self._run(lambda r: self.L.hbam_sort_split(self.ctx.h, C.byref(cols), r), cols.n_records)
 
     def sort_received(self, keys, voffset, block_size, payload):
-        """Stable sort of an exchange's receive buffers (chunks in source-rank order)."""
+        """hbam_sort_received: stable sort of an exchange's receive buffers (chunks in
+        source-rank order)."""
         n = int(keys.numel())
-        _, rec_off = self._gather(0, 0, block_size.data_ptr(), 0, n, size_only=True)  # offsets of received records
-        keys_s, perm = self._sort(keys.data_ptr(), n)
-        vo = self._permute(voffset.data_ptr(), 8, perm, n)
-        bs = self._permute(block_size.data_ptr(), 4, perm, n)
-        out, off = self._gather(payload.data_ptr(), rec_off.data_ptr(), block_size.data_ptr(),
-                                perm.data_ptr(), n)
-        return SortedRun(keys_s, vo, bs, out, off)
+        return self._run(lambda r: self.L.hbam_sort_received(
+            self.ctx.h, C.c_void_p(keys.data_ptr()), C.c_void_p(voffset.data_ptr()),
+            C.c_void_p(block_size.data_ptr()), C.c_void_p(payload.data_ptr()), n, r), n)
+
+    def partition(self, run, split_points):
+        """hbam_sort_partition: TotalOrderPartitioner record / byte bounds (host int64 arrays)."""
+        from ._lib import SortedRunC
+        sp = np.ascontiguousarray(split_points, np.int64)
+        P = len(sp) + 1
+        rb = np.zeros(P + 1, np.uint64)
+        bb = np.zeros(P + 1, np.uint64)
+        r = SortedRunC(run.n, int(run.offsets[-1].item()) if run.n else 0, run.keys.data_ptr(),
+                       run.voffset.data_ptr(), run.block_size.data_ptr(), run.offsets.data_ptr(),
+                       run.payload.data_ptr())
+        self._after_torch()
+        self._chk(self.L.hbam_sort_partition(self.ctx.h, C.byref(r), C.c_void_p(sp.ctypes.data), P,
+                                             C.c_void_p(rb.ctypes.data), C.c_void_p(bb.ctypes.data)),
+                  "hbam_sort_partition")
+        return rb.astype(np.int64), bb.astype(np.int64)
 
 
 def choose_split_points(keys_sorted, world, all_gather_fn, samples_per_rank=4096):
@@ -144,33 +152,42 @@ def choose_split_points(keys_sorted, world, all_gather_fn, samples_per_rank=4096
     return allv[q].astype(np.int64)
 
 
-def exchange(run, split_points, dist, ops):
+def exchange(run, split_points, dist, ops, stage_cpu=None):
     """all_to_all of a SortedRun by key range; returns this rank's globally-ordered run.
-    Keys <= split_points[r-1]... : rank r receives keys in (sp[r-1], sp[r]]."""
+    Rank r receives the keys in (sp[r-1], sp[r]].  With a CPU-only backend (gloo) and device
+    runs, the collective's buffers are staged through host memory (stage_cpu, default: gloo)."""
     import torch
     world = dist.get_world_size()
     dev = run.keys.device
-    sp = torch.as_tensor(np.asarray(split_points, np.int64), device=dev)
-    cuts = torch.searchsorted(run.keys, sp, right=True) if run.n else torch.zeros_like(sp)
-    bounds = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cuts.to(torch.int64),
-                        torch.full((1,), run.n, dtype=torch.int64, device=dev)])
-    rec_cnt = bounds[1:] - bounds[:-1]
-    byte_b = run.offsets[bounds]
-    byte_cnt = byte_b[1:] - byte_b[:-1]
-    meta = torch.stack([rec_cnt, byte_cnt]).t().contiguous()  # [world, 2]
+    if stage_cpu is None:
+        stage_cpu = dev.type != "cpu" and dist.get_backend() == "gloo"
+    xdev = torch.device("cpu") if stage_cpu else dev
+    if hasattr(ops, "partition"):
+        rb, bb = ops.partition(run, split_points)
+        rec_cnt = torch.as_tensor(rb[1:] - rb[:-1], dtype=torch.int64)
+        byte_cnt = torch.as_tensor(bb[1:] - bb[:-1], dtype=torch.int64)
+    else:
+        sp = torch.as_tensor(np.asarray(split_points, np.int64), device=dev)
+        cuts = torch.searchsorted(run.keys, sp, right=True) if run.n else torch.zeros_like(sp)
+        bounds = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), cuts.to(torch.int64),
+                            torch.full((1,), run.n, dtype=torch.int64, device=dev)])
+        rec_cnt = (bounds[1:] - bounds[:-1]).cpu()
+        byte_b = run.offsets[bounds]
+        byte_cnt = (byte_b[1:] - byte_b[:-1]).cpu()
+    meta = torch.stack([rec_cnt, byte_cnt]).t().contiguous().to(xdev)  # [world, 2]
     rmeta = torch.empty_like(meta)
     dist.all_to_all_single(rmeta, meta)
-    send_r = rec_cnt.cpu().tolist()
-    send_b = byte_cnt.cpu().tolist()
+    send_r = rec_cnt.tolist()
+    send_b = byte_cnt.tolist()
     rm = rmeta.cpu().numpy()
     recv_r = [int(x) for x in rm[:, 0]]
     recv_b = [int(x) for x in rm[:, 1]]
     nr, nb = sum(recv_r), sum(recv_b)
 
     def a2a(src, n_out, dtype, s_split, r_split):
-        out = torch.empty(n_out, dtype=dtype, device=dev)
-        dist.all_to_all_single(out, src.contiguous(), r_split, s_split)
-        return out
+        out = torch.empty(n_out, dtype=dtype, device=xdev)
+        dist.all_to_all_single(out, src.contiguous().to(xdev), r_split, s_split)
+        return out.to(dev)
 
     keys = a2a(run.keys, nr, torch.int64, send_r, recv_r)
     vo = a2a(run.voffset, nr, torch.int64, send_r, recv_r)

@@ -77,7 +77,9 @@ typedef struct hbam_block {
 
 /* Decoded split, struct-of-arrays.  In hbam_decode_split's output every pointer is a
  * device pointer owned by the context; after hbam_columns_to_host they are host
- * pointers owned by the caller (free with hbam_free_host_columns). */
+ * pointers owned by the caller (free with hbam_free_host_columns).  In the host copy, ubuf
+ * holds exactly the records' bytes (each record's block_size field + record, i.e. the
+ * SAMRecordWritable wire form) and rec_off is relative to it. */
 typedef struct hbam_columns {
   uint64_t n_records;
   int32_t status;       /* HBAM_OK, or the exception nextKeyValue()/initialize() raises */
@@ -152,12 +154,33 @@ int hbam_inflate(hbam_ctx* ctx, const uint8_t* comp, int on_device, uint64_t com
 
 /* ---- BAMRecordReader.initialize + nextKeyValue loop (BAMRecordReader.java:108-188)
  * over FileVirtualSplit [v_start, v_end) (FileVirtualSplit.java:38-92).
- * `comp` = bytes [comp_base, comp_base+comp_len) of a file of length file_len.
- * n_ref < 0: parse it from the header (comp must then start at file offset 0). */
+ * `comp` = bytes [comp_base, comp_base+comp_len) of a file of length file_len (a window).
+ * n_ref < 0: parse it from the header (comp must then start at file offset 0).
+ * Windows: when the window ends before the split does, out->status = HBAM_EMORE, the first
+ * n_records records are final, and voffset[n_records] (device) is the virtual offset to
+ * resume from (v_start when n_records == 0 and no column was produced: the window is too
+ * small); the next window must start at or before that offset's BGZF block.  Resuming at
+ * that offset gives exactly the records (and the exception) one whole-file call gives. */
 int hbam_decode_split(hbam_ctx* ctx, const uint8_t* comp, int on_device, uint64_t comp_base,
                       uint64_t comp_len, uint64_t file_len, uint64_t v_start, uint64_t v_end,
                       int32_t n_ref, hbam_columns* out);
 int hbam_columns_to_host(hbam_ctx* ctx, const hbam_columns* dev, hbam_columns* host);
+/* Streamed split read: BAMRecordReader over FileVirtualSplit
+ * [v_start, v_end) of a file the caller holds in host memory (e.g. mmap), decoded in windows
+ * of about window_bytes compressed bytes.  While window k decodes, the predicted window k+1
+ * is copied to the device on a second HIP stream.  hbam_split_next fills `out` (device
+ * columns, valid until the next call on the stream's context) with the next window's
+ * records and returns 1, returns 0 once the split is exhausted, <0 on a library error;
+ * out->status != HBAM_OK (never HBAM_EMORE) is the exception nextKeyValue raises after
+ * out->n_records records, and ends the stream. */
+typedef struct hbam_split_stream hbam_split_stream;
+hbam_split_stream* hbam_split_open(hbam_ctx* ctx, const uint8_t* file, uint64_t file_len,
+                              uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                              uint64_t window_bytes);
+int hbam_split_next(hbam_split_stream* s, hbam_columns* out);
+/* bytes copied host->device and the copies' wall time (ms) so far */
+int hbam_split_stats(const hbam_split_stream* s, uint64_t* h2d_bytes, double* h2d_ms, uint64_t* windows);
+void hbam_split_close(hbam_split_stream* s);
 void hbam_free_host_columns(hbam_columns* host);
 void hbam_release_columns(hbam_ctx* ctx, hbam_columns* dev);
 
@@ -200,6 +223,39 @@ int hbam_sort_keys(hbam_ctx* ctx, const int64_t* keys, uint64_t n, int64_t* keys
 int hbam_gather_records(hbam_ctx* ctx, const uint8_t* ubuf, const uint64_t* rec_off,
                         const int32_t* block_size, const uint32_t* perm, uint64_t n, uint8_t* out,
                         uint64_t out_cap, uint64_t* out_off, uint64_t* total_bytes);
+/* ---- Sort plugin, one rank's steps (Sort.java:131-170, SortRecordReader :279-295) ----------
+ * A sorted run: records in (key, input order) order with their voffsets, block sizes and packed
+ * SAMRecordWritable payloads (block_size field + record, SAMRecordWritable.java:62-63).  All
+ * pointers are caller-owned device buffers (hbam_device_alloc): call with payload == NULL
+ * first to get n and payload_bytes, then with key[n], voffset[n], block_size[n],
+ * offsets[n+1] (payload offsets) and payload[payload_bytes].  A Java host drives the plugin as
+ *   decode (hbam_decode_split) -> hbam_sort_split -> hbam_sort_partition with the
+ *   TotalOrderPartitioner split points -> its own transport of each partition's slice ->
+ *   hbam_sort_received on the concatenation of what it received (in source order).
+ * Ties keep input order, so a run is ordered by (key, file order): the documented tie-break. */
+typedef struct hbam_sorted_run {
+  uint64_t n;
+  uint64_t payload_bytes;
+  int64_t* key;
+  int64_t* voffset;
+  int32_t* block_size;
+  uint64_t* offsets;
+  uint8_t* payload;
+} hbam_sorted_run;
+int hbam_device_alloc(hbam_ctx* ctx, uint64_t bytes, void** dev_out);
+/* the records of a decoded split (device columns) as a sorted run */
+int hbam_sort_split(hbam_ctx* ctx, const hbam_columns* dv, hbam_sorted_run* out);
+/* TotalOrderPartitioner (Sort.java:149) over a sorted run: partition k (0 <= k < nparts) holds
+ * the keys in (split_points[k-1], split_points[k]] (host array of nparts-1 signed keys);
+ * rec_bounds / byte_bounds (host, nparts+1) get each partition's record and payload ranges. */
+int hbam_sort_partition(hbam_ctx* ctx, const hbam_sorted_run* run, const int64_t* split_points,
+                        uint32_t nparts, uint64_t* rec_bounds, uint64_t* byte_bounds);
+/* receive side: n records (device key/voffset/block_size and their packed payload, chunks in
+ * source-rank order) as a sorted run */
+int hbam_sort_received(hbam_ctx* ctx, const int64_t* key, const int64_t* voffset,
+                       const int32_t* block_size, const uint8_t* payload, uint64_t n,
+                       hbam_sorted_run* out);
+
 /* SplittingBAMIndexer (SplittingBAMIndexer.java:146-248, §8 f-2) from a whole-file decode
  * (dv: device columns of hbam_decode_split over [first record, len<<16|0xffff]): out (host)
  * = voffset of the first record, the voffset before every granularity-th record, then

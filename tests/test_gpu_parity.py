@@ -294,3 +294,79 @@ def test_resolve_forged_descriptor_is_an_error_not_a_hang(gpu_ctx, case):
     rc, st, _ = gpu_ctx.resolve_tokens(bytes(io), bm, *tail)
     assert rc == 0
     assert st == -7  # HBAM_EDATA
+
+
+# ---- config #4 shape: byte-range shards read through streamed windows ------------------------
+def _stream_read(gpu_ctx, data, a, z, n_ref, window):
+    """hbam_split_open/next over one FileVirtualSplit -> (concatenated columns, n windows)."""
+    ws = list(gpu_ctx.split_stream(data, int(a), int(z), n_ref, window_bytes=window))
+    cat = {"n": sum(w["n"] for w in ws), "status": 0, "err_record": 0}
+    base = 0
+    for w in ws:
+        if w["status"] != 0:
+            cat["status"] = w["status"]
+            cat["err_record"] = base + w["err_record"]
+        base += w["n"]
+    from helpers import FIELDS
+    for k in FIELDS + ("layout_ok",):
+        cat[k] = np.concatenate([w[k] for w in ws]) if ws else np.zeros(0)
+    for k in ("names", "cigars", "seq", "qual", "aux"):
+        cat[k] = np.concatenate([w[k] for w in ws]) if ws else np.zeros(0)
+    cat["payload"] = b"".join(w["ubuf"].tobytes() for w in ws)
+    return cat, len(ws)
+
+
+@pytest.mark.parametrize("name", GOLDEN_FILES)
+@pytest.mark.parametrize("P", [2, 3, 5])
+def test_sharded_split_windows_match_oracle(gpu_ctx, oracle_mod, name, P):
+    """P byte-range FileSplits of one file, aligned by the guesser (addProbabilisticSplits),
+    each read through 64 KiB streamed windows (EMORE continuation at every window end): every
+    shard equals the oracle's BAMRecordReader for that FileVirtualSplit, record bytes included;
+    without the duplicated boundary-block records the shards concatenate to the whole-file read."""
+    data = _load(name)
+    L = len(data)
+    b = np.array([L * k // P for k in range(P)], np.uint64)
+    e = np.array([L * (k + 1) // P for k in range(P)], np.uint64)
+    want = oracle_mod.probabilistic_splits(data, b, e)
+    n, vs, ve = gpu_ctx.probabilistic_splits(data, b, e)
+    if isinstance(want, int):
+        assert n == want
+        return
+    assert np.array_equal(vs, want[0]) and np.array_equal(ve, want[1])
+    h = oracle_mod.read_header(data)
+    shards = []
+    for a, z in zip(vs, ve):
+        ref = oracle_mod.read_split(data, int(a), int(z))
+        got, nwin = _stream_read(gpu_ctx, data, a, z, h["n_ref"], 64 << 10)
+        assert_same_split(got, ref)
+        assert got["payload"] == oracle_mod.record_payloads(ref)[0].tobytes()
+        assert nwin >= 2 or L // P < (64 << 10)
+        shards.append(got)
+    whole = oracle_mod.read_split(data, h["first_voffset"], _whole(data))
+    wv = set(int(x) for x in whole["voffset"])
+    if all(int(a) in wv for a in vs[1:]) and whole["status"] == 0:
+        vo = list(shards[0]["voffset"])
+        for sh in shards[1:]:
+            cut = int(np.searchsorted(sh["voffset"], vo[-1], side="right")) if vo else 0
+            vo.extend(sh["voffset"][cut:])
+        assert np.array_equal(np.array(vo, np.uint64), whole["voffset"])
+
+
+def test_windowed_decode_comp_base(gpu_ctx, oracle_mod):
+    """hbam_decode_split with comp_base != 0: a window [c, c+W) of the file decodes the same
+    records as the whole buffer up to the window's EMORE, whose voffset[n] is the resume point."""
+    data = _load("small_pe.bam")
+    h = oracle_mod.read_header(data)
+    ref = oracle_mod.read_split(data, h["first_voffset"], _whole(data))
+    k = len(ref["voffset"]) // 3
+    v0 = int(ref["voffset"][k])
+    c = v0 >> 16
+    win = data[c:c + (300 << 10)]
+    got = gpu_ctx.decode_split(np.ascontiguousarray(win), v0, _whole(data), n_ref=h["n_ref"],
+                               comp_base=c, file_len=len(data))
+    assert got["rc"] == 0
+    assert got["status"] == -12  # HBAM_EMORE
+    m = got["n"]
+    assert m > 100
+    assert np.array_equal(got["voffset"], ref["voffset"][k:k + m])
+    assert np.array_equal(got["key"], ref["key"][k:k + m])

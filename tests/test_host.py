@@ -68,3 +68,53 @@ def test_any_sam_input_format_dispatch(tmp_path):
     assert AnySAMInputFormat().getFormat(str(r)) == "BAM"
     assert AnySAMInputFormat().getFormat(str(r), Configuration({
         "hadoopbam.anysam.trust-exts": "false"})) == "SAM"
+
+
+def test_generate_range_concatenates_to_one_file(genbam, oracle_mod):
+    """Byte ranges of one synthetic file (bench.py --gpus N: one range per rank) concatenate
+    to the whole file, which the oracle reads with the generator's record count."""
+    kw = dict(seed=9, segment=400, threads=4)
+    whole = genbam.generate_range(6, 0, 6, header=True, tail=True, **kw)
+    parts = [genbam.generate_range(6, 0, 2, header=True, **kw), genbam.generate_range(6, 2, 3, **kw),
+             genbam.generate_range(6, 5, 1, tail=True, **kw)]
+    assert np.array_equal(np.concatenate(parts), whole)
+    assert sum(p.n_records for p in parts) == whole.n_records
+    h = oracle_mod.read_header(whole)
+    r = oracle_mod.read_split(whole, h["first_voffset"], (len(whole) << 16) | 0xffff)
+    assert r["status"] == 0 and r["n"] == whole.n_records
+
+
+def test_host_murmurhash3_matches_oracle(oracle_mod):
+    """formats.murmurhash3_bytes (the host getKey(SAMRecord) hash) equals the oracle's
+    MurmurHash3.murmurhash3(byte[], seed) for every tail length and negative seeds."""
+    from hadoop_bam.formats import murmurhash3_bytes
+    rng = np.random.default_rng(5)
+    for n in list(range(0, 40)) + [255, 1000]:
+        b = rng.integers(0, 256, n).astype(np.uint8).tobytes()
+        for seed in (0, 7, -3):
+            assert murmurhash3_bytes(b, seed) == oracle_mod.murmurhash3(b, seed), (n, seed)
+
+
+def test_record_bytes_fields_and_static_get_key(oracle_mod):
+    """SAMRecordWritable.readFields -> lazy record over the wire bytes: its fixed fields equal
+    the oracle's decode, and the static BAMRecordReader.getKey(SAMRecord) (Sort.java:292) equals
+    the key the reader emits, unmapped-hash keys included."""
+    from hadoop_bam import BAMRecordReader, SAMRecordWritable
+    data = np.fromfile(os.path.join(GOLDEN, "small_pe.bam"), dtype=np.uint8)
+    h = oracle_mod.read_header(data)
+    cols = oracle_mod.read_split(data, h["first_voffset"], (len(data) << 16) | 0xffff)
+    pay, off = oracle_mod.record_payloads(cols)
+    n_hash = 0
+    for i in range(0, cols["n"], 7):
+        w = SAMRecordWritable()
+        w.readFields(io.BytesIO(pay[off[i]:off[i + 1]].tobytes()))
+        r = w.get()
+        assert r.getReferenceIndex() == cols["ref_id"][i]
+        assert r.getAlignmentStart() == int(np.int32(cols["pos"][i]) + np.int32(1))
+        assert r.getFlags() == cols["flag"][i]
+        assert BAMRecordReader.getKey(r) == int(cols["key"][i])
+        n_hash += int(cols["key"][i] >> 32 == 0x7fffffff or cols["key"][i] < 0)
+        out = io.BytesIO()
+        w.write(out)
+        assert out.getvalue() == pay[off[i]:off[i + 1]].tobytes()
+    assert n_hash > 0

@@ -62,6 +62,15 @@ int hbamgen_generate_mem(const hbamgen_params* p, uint8_t** out, uint64_t* out_l
 int hbamgen_generate_file(const hbamgen_params* p, const char* path, uint64_t* out_len,
                           uint64_t* n_records_out);
 void hbamgen_free(uint8_t* p);
+// Byte range of ONE file made of `n_seg_total` main segments (target_bytes / n_records are
+// ignored): segments [seg_first, seg_first + seg_count), preceded by the header blocks when
+// flags & 1, followed by the unplaced-unmapped tail and the terminator when flags & 2.  The
+// concatenation of consecutive ranges (header on the first, tail on the last) is the file
+// hbamgen_generate_mem writes for n_records = n_seg_total * segment_records (+ the unplaced
+// tail).  Requires empty_block_every == 0 (empty blocks use a file-global block counter).
+int hbamgen_generate_range(const hbamgen_params* p, uint64_t n_seg_total, uint64_t seg_first,
+                           uint64_t seg_count, int32_t flags, uint8_t** out, uint64_t* out_len,
+                           uint64_t* n_records_out);
 }
 
 namespace {
@@ -581,6 +590,65 @@ int hbamgen_generate_file(const hbamgen_params* p, const char* path, uint64_t* o
 }
 
 void hbamgen_free(uint8_t* p) { free(p); }
+
+int hbamgen_generate_range(const hbamgen_params* p0, uint64_t n_seg_total, uint64_t seg_first,
+                           uint64_t seg_count, int32_t flags, uint8_t** out, uint64_t* out_len,
+                           uint64_t* n_records_out) {
+  hbamgen_params P = *p0;
+  if (P.empty_block_every != 0 || seg_first + seg_count > n_seg_total) return -1;
+  if (P.block_payload <= 0 || P.block_payload > 65536) P.block_payload = 65280;
+  if (P.segment_records <= 0) P.segment_records = 65536;
+  if (P.threads <= 0) P.threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (P.n_ref <= 0) P.n_ref = 25;
+  Genome g(P.n_ref);
+  const uint64_t R = (uint64_t)P.segment_records;
+  std::string acc;
+  uint64_t nrec = 0;
+  if (flags & 1) {
+    Compressor c(P.level);
+    std::string h = make_header_bytes(g, P.sorted != 0);
+    for (size_t off = 0; off < h.size(); off += (size_t)P.block_payload)
+      c.block(acc, (const uint8_t*)h.data() + off, std::min((size_t)P.block_payload, h.size() - off));
+  }
+  std::vector<std::string> outs((size_t)seg_count);
+  std::atomic<uint64_t> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < P.threads; ++t)
+    th.emplace_back([&]() {
+      Compressor c(P.level);
+      for (uint64_t k; (k = next.fetch_add(1)) < seg_count;) {
+        std::vector<uint32_t> sizes;
+        const uint64_t seg = seg_first + k;
+        std::string u = make_segment(P, g, seg, seg * R, R, false, &sizes);
+        uint64_t nb = 0;
+        outs[(size_t)k] = compress_segment(P, u, sizes, c, &nb, 0);
+      }
+    });
+  for (auto& x : th) x.join();
+  for (auto& o : outs) acc += o;
+  nrec += seg_count * R;
+  if (flags & 2) {
+    const uint64_t main_records = n_seg_total * R;
+    const uint64_t unplaced = P.sorted ? main_records * (uint64_t)P.unplaced_permille / 1000 : 0;
+    for (uint64_t first = 0; first < unplaced; first += R) {
+      const uint64_t cnt = std::min(R, unplaced - first);
+      Compressor c(P.level);
+      std::vector<uint32_t> sizes;
+      std::string u = make_segment(P, g, 0x7fff0000ULL + first / R, main_records, cnt, true, &sizes);
+      uint64_t nb = 0;
+      acc += compress_segment(P, u, sizes, c, &nb, 0);
+      nrec += cnt;
+    }
+    if (P.write_terminator) acc.append((const char*)kEof, 28);
+  }
+  uint8_t* buf = (uint8_t*)malloc(acc.size() ? acc.size() : 1);
+  if (!buf) return -1;
+  memcpy(buf, acc.data(), acc.size());
+  *out = buf;
+  *out_len = acc.size();
+  if (n_records_out) *n_records_out = nrec;
+  return 0;
+}
 
 }  // extern "C"
 

@@ -38,6 +38,10 @@ def lib():
         L.hbamgen_generate_file.argtypes = [C.POINTER(Params), C.c_char_p,
                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.hbamgen_free.argtypes = [C.POINTER(C.c_uint8)]
+        L.hbamgen_generate_range.argtypes = [C.POINTER(Params), C.c_uint64, C.c_uint64, C.c_uint64,
+                                             C.c_int32, C.POINTER(C.POINTER(C.c_uint8)),
+                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.hbamgen_generate_range.restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -95,3 +99,21 @@ class GenBam(np.ndarray):
 
     def __array_finalize__(self, obj):
         self.n_records = getattr(obj, "n_records", 0)
+
+
+def generate_range(n_seg_total, seg_first, seg_count, header=False, tail=False, **kw):
+    """Bytes of segments [seg_first, seg_first+seg_count) of ONE file of n_seg_total main
+    segments (+ the header blocks / the unplaced tail and terminator): consecutive ranges
+    concatenate to that file, so ranks can each hold their byte range of it."""
+    p = params(**kw)
+    out = C.POINTER(C.c_uint8)()
+    n = C.c_uint64(0)
+    nrec = C.c_uint64(0)
+    rc = lib().hbamgen_generate_range(C.byref(p), n_seg_total, seg_first, seg_count,
+                                      (1 if header else 0) | (2 if tail else 0), C.byref(out),
+                                      C.byref(n), C.byref(nrec))
+    if rc:
+        raise ValueError("hbamgen_generate_range failed (empty_every must be 0)")
+    a = np.ctypeslib.as_array(out, shape=(n.value,)).copy() if n.value else np.zeros(0, np.uint8)
+    lib().hbamgen_free(out)
+    return GenBam(a, nrec.value)
