@@ -26,6 +26,10 @@
 
 using namespace hbam;
 
+#ifndef HBAM_GUESS_BATCH
+#define HBAM_GUESS_BATCH 16384  // guesses per launch (~66 KiB of scratch + the window cache each)
+#endif
+
 namespace {
 
 struct Buf {
@@ -126,6 +130,7 @@ struct hbam_ctx {
   hipEvent_t ev[16];
   hbam_timing timing{};
   uint64_t* pinned_small = nullptr;  // host pinned scalars
+  uint64_t guess_batch = HBAM_GUESS_BATCH;  // env HBAM_GUESS_BATCH overrides (tests: multi-batch)
 };
 
 namespace {
@@ -175,9 +180,6 @@ int ensure(hbam_ctx* c, BufId id, size_t count, T** out) {
 }
 
 float ev_ms(hbam_ctx* c, int a, int b);
-#ifndef HBAM_GUESS_BATCH
-#define HBAM_GUESS_BATCH 16384  // guesses per launch (~64 KiB + cache each); config #3 A/B: 4096 -> 1.50 s, 16384 -> 0.094 s
-#endif
 inline uint32_t grid_for(uint64_t n, uint32_t wg) { return (uint32_t)((n + wg - 1) / wg); }
 
 // stream-ordered synchronous copy (the context stream is non-blocking: a plain hipMemcpy
@@ -425,6 +427,10 @@ hbam_ctx* hbam_create(int device_ordinal, const hbam_opts* opts) {
     return nullptr;
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
+  if (const char* gb = getenv("HBAM_GUESS_BATCH")) {
+    const long v = strtol(gb, nullptr, 10);
+    if (v > 0) c->guess_batch = (uint64_t)v;
+  }
   if (hipHostMalloc((void**)&c->pinned_small, 4096, hipHostMallocDefault) != hipSuccess) {
     delete c;
     return nullptr;
@@ -894,7 +900,7 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if ((rc = ensure(c, B_RECOFF, nrec + 1, &rec_off))) return rc;
   if ((rc = ensure(c, B_VOFF, nrec + 1, &voff))) return rc;
   k_emit_offsets<<<(uint32_t)wb, 256, 0, c->stream>>>(uo, blk + sblk, (uint32_t)wb, rel, count, rbase,
-                                                      rec_off, voff);
+                                                      comp_base, rec_off, voff);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
 
@@ -1345,25 +1351,38 @@ extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device,
     }
   }
   HIPCHK(c, hipEventRecord(c->ev[9], c->stream));
-  const uint64_t batch = HBAM_GUESS_BATCH;
-  for (uint64_t g0 = 0; g0 < k; g0 += batch) {
+  uint64_t batch = c->guess_batch;
+  for (uint64_t g0 = 0; g0 < k;) {
     const uint64_t kb = std::min(batch, k - g0);
     GuessWork w;
-    if ((rc = guess_work(c, kb, &w))) return rc;
+    if ((rc = guess_work(c, kb, &w))) {
+      if (rc == HBAM_ENOMEM && kb > 1) {  // back off: half the guesses per launch
+        batch = (kb + 1) / 2;
+        continue;
+      }
+      return rc;
+    }
     std::vector<uint8_t> ib(kb * 8);
     for (uint64_t i = 0; i < kb; ++i) memcpy(&ib[i * 8], magic, 8);
     HIPCHK(c, hipMemcpyAsync(w.bufs, ib.data(), kb * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(w.beg, beg + g0, kb * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(w.end, end + g0, kb * 8, hipMemcpyHostToDevice, c->stream));
     GuessCache gc;
-    if ((rc = build_guess_cache(c, d, file_len, w.beg, w.end, kb, &gc))) return rc;
-    k_guess_bam<<<grid_for(kb, GUESS_BAM_WG), GUESS_BAM_WG, 0, c->stream>>>(
+    if ((rc = build_guess_cache(c, d, file_len, w.beg, w.end, kb, &gc))) {
+      if (rc == HBAM_ENOMEM && kb > 1) {
+        batch = (kb + 1) / 2;
+        continue;
+      }
+      return rc;
+    }
+    k_guess_bam_wave<<<(uint32_t)kb, 64, 0, c->stream>>>(
         d, (int64_t)file_len, w.beg, w.end, (uint32_t)kb, n_ref, w.scratch, w.lens, w.bufs, w.out,
         w.err, gc.cn, gc.cbase, gc.cpos, gc.cblk, gc.cuoff, gc.cubuf, gc.cst, gc.ccrc);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(out + g0, w.out, kb * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(err + g0, w.err, kb * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    g0 += kb;
   }
   HIPCHK(c, hipEventRecord(c->ev[10], c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1761,5 +1780,9 @@ extern "C" int hbam_resolve_tokens(hbam_ctx* c, uint8_t* io, uint32_t isize, con
 extern "C" int hbam_prof_attach(void* dev) {
   unsigned long long* p = (unsigned long long*)dev;
   return hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_prof), &p, sizeof p) == hipSuccess ? 0 : -1;
+}
+extern "C" int hbam_prof_attach_guess(void* dev) {
+  unsigned long long* p = (unsigned long long*)dev;
+  return hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_gprof), &p, sizeof p) == hipSuccess ? 0 : -1;
 }
 #endif

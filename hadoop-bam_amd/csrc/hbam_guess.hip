@@ -1,8 +1,8 @@
 // hbam_guess.hip — BAMSplitGuesser / BGZFSplitGuesser on the device (gfx950).
 //
-// One lane = one guesser call guessNextBAMRecordStart(beg, end) (BAMSplitGuesser.java:109-212),
+// One wave = one guesser call guessNextBAMRecordStart(beg, end) (BAMSplitGuesser.java:109-212),
 // so BAMInputFormat.addProbabilisticSplits' per-split loop (BAMInputFormat.java:181-222) and
-// config #3's 10k guesses run as one launch.  The lane runs the reference's state machine
+// config #3's 10k guesses run as one launch.  The wave runs the reference's state machine
 // over the window W = file[beg, beg+min(end-beg, 262139)) with the same cursor semantics the
 // Java code observes:
 //   * SeekableArrayStream (util/SeekableArrayStream.java:29-58) — one shared position used by
@@ -30,13 +30,6 @@ constexpr int32_t G_MAGIC = 0x04088b1f;
 constexpr int32_t G_MAGIC_SUB = 0x00024342;
 constexpr int32_t G_MAX_BYTES_READ = 3 * 0xffff + 0xfffe;
 constexpr uint32_t GUESS_WG = 64;
-#ifndef HBAM_GUESS_BAM_WG
-#define HBAM_GUESS_BAM_WG 64
-#endif
-// lanes (= guesses) per k_guess_bam workgroup.  A/B on config #3 (10k guesses, 2 GB file):
-// 64 -> 1.52 s, 8 -> 1.51 s, 4 -> 1.48 s: spreading guesses over more SIMDs does not help, the
-// batch time is set by its slowest guesses, so the default stays 64.
-constexpr uint32_t GUESS_BAM_WG = HBAM_GUESS_BAM_WG;
 constexpr uint32_t GC_CAP = 256;      // cached candidate blocks per guess window
 
 // Candidate blocks of one guess window (sorted absolute file offsets) and their inflated
@@ -343,62 +336,6 @@ __device__ int32_t g_next_bam(Guesser& g, uint64_t cpv, int32_t up, int32_t csiz
   return -1;
 }
 
-// guessNextBAMRecordStart :109-212
-__device__ int64_t g_guess(Guesser& g, const uint8_t* file, int64_t flen, int64_t beg, int64_t end,
-                           int32_t* err) {
-  *err = HBAM_OK;
-  int32_t want = (int32_t)(end - beg);
-  if (want > G_MAX_BYTES_READ) want = G_MAX_BYTES_READ;
-  int64_t total = 0;
-  if (want > 0 && beg >= 0 && beg <= flen) total = (flen - beg < want) ? flen - beg : want;
-  g.in.a = file + ((beg >= 0 && beg <= flen) ? beg : 0);
-  g.in.len = total;
-  g.in.pos = 0;
-  g.bz.wbase = (beg >= 0 && beg <= flen) ? beg : 0;
-  g.bz.block_addr = 0;
-  g.bz.last_len = 0;
-  g.bz.cur_len = -1;
-  g.bz.cur_off = 0;
-  int32_t first_end = (int32_t)(end - beg);
-  if (first_end > 0xffff) first_end = 0xffff;
-  for (int32_t cp = 0;; ++cp) {
-    int32_t ppos, psize;
-    if (!g_next_bgzf(g, cp, first_end, &ppos, &psize)) return end;
-    const int32_t cp0 = cp = ppos;
-    const uint64_t cpv = (uint64_t)(uint32_t)cp0 << 16;
-    if (gb_seek(g.bz, g.in, cpv)) continue;  // catch (Throwable)
-    for (int32_t up = 0;; ++up) {
-      const int32_t up0 = up = g_next_bam(g, cpv, up, psize);
-      if (up0 < 0) break;
-      if (gb_seek(g.bz, g.in, cpv | (uint32_t)up0)) { *err = HBAM_EIO; return end; }
-      bool decoded_any = false;
-      int b = 0;
-      int32_t prev = cp0;
-      int32_t rc = 0;
-      while (b < 3) {
-        rc = gc_decode(g.bz, g.in);
-        if (rc <= 0) break;
-        decoded_any = true;
-        const int32_t cp2 = (int32_t)(gb_tell(g.bz) >> 16);
-        if (cp2 != prev) { prev = cp2; ++b; }
-      }
-      if (rc < 0) {
-        if (rc == HBAM_EFORMAT || rc == HBAM_ETRUNC || rc == HBAM_ERUNTIMEIO || rc == HBAM_EREFID)
-          continue;
-        if (rc == HBAM_EEOF) {
-          if (!decoded_any && g.in.pos == g.in.len) continue;
-        } else {
-          *err = rc;
-          return end;
-        }
-      } else if (b < 3) {
-        if (!decoded_any) continue;
-      }
-      return (int64_t)((uint64_t)(beg + cp0) << 16 | (uint32_t)up0);
-    }
-  }
-}
-
 // Candidate blocks of each guess window: every offset of the window (the bytes
 // BAMSplitGuesser's stream can reach, :118-126) that starts with the gzip magic 1f 8b 08 04.
 // One workgroup per window; sorted by rank; count > GC_CAP marks the window uncached.
@@ -494,28 +431,253 @@ __device__ void crc_table_init(uint32_t* T) {
   __syncthreads();
 }
 
-// One lane per guess.  bufs[i] = initial 8-byte ByteBuffer state; written back at exit.
-__global__ __launch_bounds__(GUESS_BAM_WG) void k_guess_bam(const uint8_t* __restrict__ file, int64_t flen,
-                                                        const int64_t* __restrict__ beg,
-                                                        const int64_t* __restrict__ end, uint32_t k,
-                                                        int32_t n_ref, uint8_t* __restrict__ scratch,
-                                                        uint8_t* __restrict__ lens_scratch,
-                                                        uint8_t* __restrict__ bufs,
-                                                        int64_t* __restrict__ out,
-                                                        int32_t* __restrict__ err,
-                                                        const uint32_t* __restrict__ cn,
-                                                        const uint64_t* __restrict__ cbase,
-                                                        const uint64_t* __restrict__ cpos,
-                                                        const BlockRec* __restrict__ cblk,
-                                                        const uint64_t* __restrict__ cuoff,
-                                                        const uint8_t* __restrict__ cubuf,
-                                                        const int32_t* __restrict__ cst,
-                                                        const uint32_t* __restrict__ ccrc) {
-  __shared__ uint16_t s_ll[GUESS_BAM_WG * 288];
-  __shared__ uint8_t s_d[GUESS_BAM_WG * 32];
+// ------------------------------------------------------------------------------------------
+// One WAVE per guess (k_guess_bam_wave): the reference state machine above still runs, in
+// lockstep on every lane (uniform values, so each load is one request), but its two byte-by-byte
+// searches are answered by the wave in parallel:
+//   * guessNextBGZFPos' magic scan (:229-247): the window's magic positions in [0, firstEnd]
+//     are listed once by 64 lanes; the scan's result from p is the first listed position q >= p
+//     with q < firstEnd or q == p (the skip rule never steps over a magic, and the end test
+//     only follows an advance).  Windows shorter than firstEnd + 4 (where a 4-byte read can be
+//     short and leave stale bytes in `buf`) take the lane-serial path.
+//   * guessNextBAMPos' candidate loop (:301-398): bam_pred() is the loop's test as a pure
+//     function of the inflated block (every read lies inside it), evaluated for 64 offsets at
+//     a time.  The serial g_next_bam is then run on the accepted offset (or the last one
+//     tested) alone, which leaves the stream, the BlockCompressedInputStream and the 8-byte
+//     buffer exactly as the full serial loop would.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t GW_MAG = 512;  // magic positions listed per window (more: lane-serial path)
+
+__device__ __forceinline__ int32_t le32(const uint8_t* u, int32_t o) {
+  return (int32_t)((uint32_t)u[o] | (uint32_t)u[o + 1] << 8 | (uint32_t)u[o + 2] << 16 |
+                   (uint32_t)u[o + 3] << 24);
+}
+// guessNextBAMPos' test at candidate c (needs c + 39 < csize): refID/pos, mate refID/pos in
+// [-1, n_ref] / >= -1, NUL at the end of the read name, block_size >= the fixed lengths
+__device__ __forceinline__ bool bam_pred(const uint8_t* u, int32_t c, int32_t csize, int32_t n_ref) {
+  const int32_t id = le32(u, c + 4), pos = le32(u, c + 8);
+  if (id < -1 || id > n_ref || pos < -1) return false;
+  const int32_t nid = le32(u, c + 24), npos = le32(u, c + 28);
+  if (nid < -1 || nid > n_ref || npos < -1) return false;
+  const int32_t name_len = u[c + 12];
+  const int32_t nul = c + 36 + name_len - 1;
+  if (nul >= csize || u[nul] != 0) return false;
+  int32_t zero_min = 32 + name_len;
+  zero_min = (int32_t)((uint32_t)zero_min + (uint32_t)(u[c + 16] | u[c + 17] << 8) * 4u);
+  const int32_t ls = le32(u, c + 20);
+  const int32_t half = (int32_t)((uint32_t)ls + 1u) / 2;
+  zero_min = (int32_t)((uint32_t)zero_min + (uint32_t)ls + (uint32_t)half);
+  return le32(u, c) >= zero_min;
+}
+
+// guessNextBGZFPos from p with the magic scan answered by the wave's list (see above)
+__device__ bool g_next_bgzf_listed(Guesser& g, int32_t p, int32_t end, const int32_t* mag,
+                                   uint32_t nmag, int32_t* opos, int32_t* osize) {
+  for (;;) {
+    if (!gs_seek(g.in, p)) return false;
+    uint32_t lo = 0, hi = nmag;  // first listed position >= p
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (mag[mid] < p) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo == nmag) return false;
+    const int32_t q = mag[lo];
+    if (q != p && q >= end) return false;
+    p = q;
+    gs_seek(g.in, p);
+    gs_read(g.in, g.buf, 4);  // the read that matched: buf = the magic, pos = p + 4
+    const int32_t p0 = p;
+    p += 10;
+    if (!gs_seek(g.in, p)) return false;
+    gs_read(g.in, g.buf, 2);
+    p += 2;
+    const int32_t xlen = gbuf_u16(g, 0);
+    const int32_t sub_end = p + xlen;
+    while (p < sub_end) {
+      gs_read(g.in, g.buf, 4);
+      if (gbuf_i32(g, 0) != G_MAGIC_SUB) {
+        p += 4 + gbuf_u16(g, 2);
+        if (!gs_seek(g.in, p)) return false;
+        continue;
+      }
+      gs_read(g.in, g.buf, 2);
+      const int32_t bsize = gbuf_u16(g, 0);
+      p += 6;
+      while (p < sub_end) {
+        if (!gs_seek(g.in, p)) return false;
+        gs_read(g.in, g.buf, 4);
+        p += 4 + gbuf_u16(g, 2);
+      }
+      if (p != sub_end) break;
+      p += bsize - xlen - 19 + 4;
+      if (!gs_seek(g.in, p)) return false;
+      gs_read(g.in, g.buf, 4);
+      *opos = p0;
+      *osize = gbuf_i32(g, 0);
+      return true;
+    }
+    p = p0 + 4;
+  }
+}
+
+// guessNextBAMPos(cpv, up, csize) with the candidate loop evaluated by the wave
+__device__ int32_t g_next_bam_wave(Guesser& g, uint64_t cpv, int32_t up, int32_t csize, uint32_t lane) {
+  if (up + 39 >= csize) return -1;  // the serial loop would not read at all
+  // the serial loop's first seek (re-reads the block if the BCIS moved on)
+  if (gb_seek(g.bz, g.in, cpv | (uint32_t)(up + 4))) return -1;
+  const uint8_t* u = g.bz.cur;
+  const int32_t last = csize - 40;
+  for (int32_t c0 = up; c0 <= last; c0 += 64) {
+    const int32_t c = c0 + (int32_t)lane;
+    const bool ok = c <= last && bam_pred(u, c, csize, g.n_ref);
+    const uint64_t m = __ballot(ok);
+    if (m) {
+      const int32_t hit = c0 + (int32_t)(__ffsll((unsigned long long)m) - 1);
+      return g_next_bam(g, cpv, hit, csize);  // == hit, with the serial loop's side effects
+    }
+  }
+  return g_next_bam(g, cpv, last, csize);  // == -1; buf / cursor as after the last test
+}
+
+// guessNextBAMRecordStart :109-212, one wave
+#ifdef HBAM_PROF
+#define GP_T(i)                                          \
+  do {                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
+    gp[i] += t_ - gq;                                    \
+    gq = t_;                                             \
+  } while (0)
+#define GP_C(i) (++gp[i])
+#else
+#define GP_T(i) \
+  do {          \
+  } while (0)
+#define GP_C(i) (void)0
+#endif
+__device__ int64_t g_guess_wave(Guesser& g, const uint8_t* file, int64_t flen, int64_t beg, int64_t end,
+                                int32_t* err, int32_t* s_mag, uint32_t* s_nmag, uint32_t lane
+#ifdef HBAM_PROF
+                                , uint64_t* gp
+#endif
+                                ) {
+#ifdef HBAM_PROF
+  uint64_t gq = __builtin_amdgcn_s_memtime();
+#endif
+  *err = HBAM_OK;
+  int32_t want = (int32_t)(end - beg);
+  if (want > G_MAX_BYTES_READ) want = G_MAX_BYTES_READ;
+  int64_t total = 0;
+  if (want > 0 && beg >= 0 && beg <= flen) total = (flen - beg < want) ? flen - beg : want;
+  g.in.a = file + ((beg >= 0 && beg <= flen) ? beg : 0);
+  g.in.len = total;
+  g.in.pos = 0;
+  g.bz.wbase = (beg >= 0 && beg <= flen) ? beg : 0;
+  g.bz.block_addr = 0;
+  g.bz.last_len = 0;
+  g.bz.cur_len = -1;
+  g.bz.cur_off = 0;
+  int32_t first_end = (int32_t)(end - beg);
+  if (first_end > 0xffff) first_end = 0xffff;
+  // list the window's magic positions in [0, first_end] (in order)
+  bool listed = first_end >= 0 && total >= (int64_t)first_end + 4;
+  if (listed) {
+    if (lane == 0) *s_nmag = 0;
+    __syncthreads();
+    uint32_t n = 0;
+    for (int32_t p0 = 0; p0 <= first_end; p0 += 64) {
+      const int32_t p = p0 + (int32_t)lane;
+      const bool mm = p <= first_end && g.in.a[p] == 0x1f && g.in.a[p + 1] == 0x8b &&
+                      g.in.a[p + 2] == 8 && g.in.a[p + 3] == 4;
+      const uint64_t bm = __ballot(mm);
+      if (mm) {
+        const uint32_t k = n + lane_rank(bm);
+        if (k < GW_MAG) s_mag[k] = p;
+      }
+      n += (uint32_t)__popcll(bm);
+    }
+    listed = n <= GW_MAG;
+    if (lane == 0) *s_nmag = n;
+    __syncthreads();
+  }
+  const uint32_t nmag = listed ? *s_nmag : 0u;
+#ifdef HBAM_PROF
+  gp[7] = listed ? nmag : 100000u;
+#endif
+  GP_T(0);  // magic listing
+  for (int32_t cp = 0;; ++cp) {
+    int32_t ppos, psize;
+    GP_C(4);
+    const bool found = listed ? g_next_bgzf_listed(g, cp, first_end, s_mag, nmag, &ppos, &psize)
+                              : g_next_bgzf(g, cp, first_end, &ppos, &psize);
+    GP_T(1);
+    if (!found) return end;
+    const int32_t cp0 = cp = ppos;
+    const uint64_t cpv = (uint64_t)(uint32_t)cp0 << 16;
+    if (gb_seek(g.bz, g.in, cpv)) continue;  // catch (Throwable)
+    GP_T(1);
+    for (int32_t up = 0;; ++up) {
+      GP_C(5);
+      const int32_t up0 = up = g_next_bam_wave(g, cpv, up, psize, lane);
+      GP_T(2);
+      if (up0 < 0) break;
+      if (gb_seek(g.bz, g.in, cpv | (uint32_t)up0)) { *err = HBAM_EIO; return end; }
+      bool decoded_any = false;
+      int b = 0;
+      int32_t prev = cp0;
+      int32_t rc = 0;
+      while (b < 3) {
+        rc = gc_decode(g.bz, g.in);
+        GP_C(6);
+        if (rc <= 0) break;
+        decoded_any = true;
+        const int32_t cp2 = (int32_t)(gb_tell(g.bz) >> 16);
+        if (cp2 != prev) { prev = cp2; ++b; }
+      }
+      GP_T(3);
+      if (rc < 0) {
+        if (rc == HBAM_EFORMAT || rc == HBAM_ETRUNC || rc == HBAM_ERUNTIMEIO || rc == HBAM_EREFID)
+          continue;
+        if (rc == HBAM_EEOF) {
+          if (!decoded_any && g.in.pos == g.in.len) continue;
+        } else {
+          *err = rc;
+          return end;
+        }
+      } else if (b < 3) {
+        if (!decoded_any) continue;
+      }
+      return (int64_t)((uint64_t)(beg + cp0) << 16 | (uint32_t)up0);
+    }
+  }
+}
+
+#ifdef HBAM_PROF
+__device__ unsigned long long* g_gprof = nullptr;  // 8 u64 per guess (tools/prof_guess.py)
+#endif
+__global__ __launch_bounds__(64) void k_guess_bam_wave(const uint8_t* __restrict__ file, int64_t flen,
+                                                       const int64_t* __restrict__ beg,
+                                                       const int64_t* __restrict__ end, uint32_t k,
+                                                       int32_t n_ref, uint8_t* __restrict__ scratch,
+                                                       uint8_t* __restrict__ lens_scratch,
+                                                       uint8_t* __restrict__ bufs,
+                                                       int64_t* __restrict__ out,
+                                                       int32_t* __restrict__ err,
+                                                       const uint32_t* __restrict__ cn,
+                                                       const uint64_t* __restrict__ cbase,
+                                                       const uint64_t* __restrict__ cpos,
+                                                       const BlockRec* __restrict__ cblk,
+                                                       const uint64_t* __restrict__ cuoff,
+                                                       const uint8_t* __restrict__ cubuf,
+                                                       const int32_t* __restrict__ cst,
+                                                       const uint32_t* __restrict__ ccrc) {
+  __shared__ uint16_t s_ll[288];
+  __shared__ uint8_t s_d[32];
   __shared__ uint32_t T[256];
+  __shared__ int32_t s_mag[GW_MAG];
+  __shared__ uint32_t s_nmag;
   crc_table_init(T);
-  const uint32_t i = blockIdx.x * GUESS_BAM_WG + threadIdx.x;
+  const uint32_t i = blockIdx.x, lane = threadIdx.x;
   if (i >= k) return;
   Guesser g;
   g.n_ref = n_ref;
@@ -533,15 +695,28 @@ __global__ __launch_bounds__(GUESS_BAM_WG) void k_guess_bam(const uint8_t* __res
     g.bz.cache.st = cst + o;
     g.bz.cache.crc = ccrc + o;
   }
-  g.bz.s_ll = s_ll + threadIdx.x * 288;
-  g.bz.s_d = s_d + threadIdx.x * 32;
+  g.bz.s_ll = s_ll;
+  g.bz.s_d = s_d;
   g.bz.lens = lens_scratch + (uint64_t)i * LENS_SLOT;
   g.bz.crc_tab = T;
   g.bz.check_crc = 1;
   int32_t e;
-  out[i] = g_guess(g, file, flen, beg[i], end[i], &e);
-  err[i] = e;
-  for (int j = 0; j < 8; ++j) bufs[8 * (uint64_t)i + j] = g.buf[j];
+#ifdef HBAM_PROF
+  uint64_t gp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  const int64_t r = g_guess_wave(g, file, flen, beg[i], end[i], &e, s_mag, &s_nmag, lane, gp);
+  if (g_gprof && lane == 0) {
+    gp[0] = __builtin_amdgcn_s_memtime() - t0;  // slot 0: whole guess (listing folded in below)
+    for (int q = 0; q < 8; ++q) g_gprof[8 * (uint64_t)i + q] = gp[q];
+  }
+#else
+  const int64_t r = g_guess_wave(g, file, flen, beg[i], end[i], &e, s_mag, &s_nmag, lane);
+#endif
+  if (lane == 0) {
+    out[i] = r;
+    err[i] = e;
+    for (int j = 0; j < 8; ++j) bufs[8 * (uint64_t)i + j] = g.buf[j];
+  }
 }
 
 // BGZFSplitGuesser.guessNextBGZFBlockStart :51-92 (its own scan :95-148, IOExceptions escape)

@@ -175,17 +175,30 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
   } else {
     TSink sink;
     sink.init(ubuf, uoff[b], r.isize, bitmap + (uint64_t)b * BITMAP_WORDS, tails + 2 * (uint64_t)b);
+#ifdef HBAM_PROF
+    uint64_t pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pc[4] = {0, 0, 0, 0};
+#endif
     st = inflate_tokens_block(comp + r.coff + 18, r.clen - 26u, r.isize, s_ll + threadIdx.x * 288,
                               s_d + threadIdx.x * 32, lens_scratch + (uint64_t)b * LENS_SLOT, sink,
-                              &produced);
+                              &produced
+#ifdef HBAM_PROF
+                              , pt, pc
+#endif
+                              );
+#ifdef HBAM_PROF
+    if (g_prof) {
+      for (int q = 0; q < 8; ++q) g_prof[32 * (uint64_t)b + 16 + q] = pt[q];
+      for (int q = 0; q < 4; ++q) g_prof[32 * (uint64_t)b + 24 + q] = pc[q];
+    }
+#endif
   }
   status[b] = st;
 #ifdef HBAM_PROF
   if (g_prof) {
-    g_prof[16 * (uint64_t)b + 8] = pr0;
-    g_prof[16 * (uint64_t)b + 9] = PROF_RT();
-    g_prof[16 * (uint64_t)b + 10] = PROF_CLK() - pc0;
-    g_prof[16 * (uint64_t)b + 11] = produced;
+    g_prof[32 * (uint64_t)b + 8] = pr0;
+    g_prof[32 * (uint64_t)b + 9] = PROF_RT();
+    g_prof[32 * (uint64_t)b + 10] = PROF_CLK() - pc0;
+    g_prof[32 * (uint64_t)b + 11] = produced;
   }
 #endif
 }
@@ -394,7 +407,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
   }
 #ifdef HBAM_PROF
   if (g_prof && lane == 0) {
-    unsigned long long* g = g_prof + 16 * (uint64_t)b;
+    unsigned long long* g = g_prof + 32 * (uint64_t)b;
     g[0] = pr0;
     g[1] = PROF_RT();
     g[2] = PROF_CLK() - pc0;
@@ -579,16 +592,19 @@ __global__ void k_chain_fix(const uint8_t* __restrict__ u, const uint64_t* __res
   }
 }
 
+// voffsets are FILE virtual offsets: block coffs are relative to the window, which starts at
+// file offset comp_base
 __global__ void k_emit_offsets(const uint64_t* __restrict__ uoff, const BlockRec* __restrict__ blk,
                                uint32_t nblk, const uint16_t* __restrict__ rel,
                                const uint32_t* __restrict__ count, const uint64_t* __restrict__ base,
-                               uint64_t* __restrict__ rec_off, uint64_t* __restrict__ voffset) {
+                               uint64_t comp_base, uint64_t* __restrict__ rec_off,
+                               uint64_t* __restrict__ voffset) {
   const uint32_t b = blockIdx.x;
   if (b >= nblk) return;
   const uint32_t n = count[b] < WALK_CAP ? count[b] : WALK_CAP;
   const uint64_t o = base[b];
   const uint64_t u0 = uoff[b];
-  const uint64_t cv = blk[b].coff << 16;
+  const uint64_t cv = (blk[b].coff + comp_base) << 16;
   for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
     const uint32_t r = rel[(uint64_t)b * WALK_CAP + k];
     rec_off[o + k] = u0 + r;

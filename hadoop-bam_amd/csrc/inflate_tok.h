@@ -28,6 +28,22 @@
 
 namespace hbam {
 
+#ifdef HBAM_PROF
+// Profiling build only: wave-level cycles per region of the Huffman pass (tools/prof_regions.py)
+#define TOK_PT(i)                                   \
+  do {                                              \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    pt[i] += t_ - tq;                               \
+    tq = t_;                                        \
+  } while (0)
+#define TOK_PC(i) (++pc[i])
+#else
+#define TOK_PT(i) \
+  do {            \
+  } while (0)
+#define TOK_PC(i) (void)0
+#endif
+
 #ifndef HBAM_TOK_K
 #define HBAM_TOK_K 4  // symbol-loop iterations per input epoch (power of two)
 #endif
@@ -142,6 +158,9 @@ struct TSink {
   uint32_t nwin;    // windows covering the block
   uint32_t w0, w1, w2, w3;
   uint32_t* tail;   // [0] = op | n<<16 | 1<<31 for a final match shorter than 3 bytes, [1] = dist
+#ifdef HBAM_AB_NOSTORE
+  uint64_t ab = 0;
+#endif
 
   __device__ __forceinline__ void init(uint8_t* ubuf, uint64_t start, uint32_t isize, uint32_t* bmp,
                                        uint32_t* tl) {
@@ -160,6 +179,10 @@ struct TSink {
   __device__ __forceinline__ void flush() {
     if (curc == ~0u) return;
     const uint32_t r0 = curc << 4;
+#ifdef HBAM_AB_NOSTORE
+    ab ^= lo ^ (hi << 1) ^ r0;  // A/B build only: output stores replaced by a register fold
+    return;
+#endif
     if (r0 >= soff && r0 + 16u <= iend) {
       const uint4 v = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
       st_out((uint4*)(cbase + r0), v);
@@ -179,6 +202,10 @@ struct TSink {
     }
   }
   __device__ __forceinline__ void win_store() {
+#ifdef HBAM_AB_NOSTORE
+    ab += w0 ^ w1 ^ w2 ^ w3;
+    return;
+#endif
     st_out((uint4*)(bm + 4u * bwin), make_uint4(w0, w1, w2, w3));
   }
   __device__ __forceinline__ void mark(uint32_t op) {
@@ -233,6 +260,9 @@ struct TSink {
       w0 = w1 = w2 = w3 = 0;
       ++bwin;
     }
+#ifdef HBAM_AB_NOSTORE
+    if (iend > soff) cbase[soff] = (uint8_t)(ab ^ (ab >> 13) ^ (ab >> 41));
+#endif
   }
 };
 
@@ -332,7 +362,14 @@ __device__ __attribute__((noinline)) bool tok_build(const uint8_t* __restrict__ 
 __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restrict__ cdata, uint32_t nbytes,
                                         uint32_t isize, uint8_t* __restrict__ syms_ll,
                                         uint8_t* __restrict__ syms_d, uint8_t* __restrict__ lens,
-                                        TSink& sink, uint32_t* produced) {
+                                        TSink& sink, uint32_t* produced
+#ifdef HBAM_PROF
+                                        , uint64_t* pt, uint64_t* pc
+#endif
+                                        ) {
+#ifdef HBAM_PROF
+  uint64_t tq = __builtin_amdgcn_s_memtime();
+#endif
   EIn in;
   ein_init(in, cdata, nbytes);
   uint32_t op = 0;
@@ -476,9 +513,56 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
     // the iteration's own output stores.
     __builtin_amdgcn_s_waitcnt(0);
     // ---- symbols of a Huffman-coded block
+    TOK_PT(6);  // header + tables
     for (;;) {
+      TOK_PC(0);
       if ((++it & (TOK_K - 1u)) == 0u) ein_epoch(in);
-      if (ein_short(in, 48)) continue;  // stall until the next epoch merges more input
+      if (ein_short(in, 48)) {
+        TOK_PC(1);
+        TOK_PT(0);
+        continue;  // stall until the next epoch merges more input
+      }
+      TOK_PT(0);
+      if (in.total - in.consumed >= 48u && op + 258u <= isize) {
+        // Fast path: at least one whole lit/len + distance's bits left in the stream and room
+        // for the longest match, so none of zlib's end-of-input / end-of-output outcomes can
+        // occur in this iteration and their checks are skipped.
+        ein_refill(in);
+        uint32_t L, hi = 0;
+        int32_t idx;
+        if (!huff_lookup_hi(hl, ein_rev15(in), L, idx, hi)) { rc = INF_DATA; goto done; }
+        const uint32_t sym = (uint32_t)syms_ll[idx] | hi;
+        ein_drop(in, L);
+        TOK_PT(1);
+        if (sym < 256u) {
+          sink.literal(op++, sym);
+          TOK_PT(2);
+          continue;
+        }
+        if (sym == 256u) break;
+        if (sym > 285u) { rc = INF_DATA; goto done; }
+        uint32_t lbase, lext;
+        length_base(sym, lbase, lext);
+        const uint32_t mlen = lbase + ein_peek(in, lext);
+        ein_drop(in, lext);
+        ein_refill(in);
+        TOK_PT(3);
+        if (!huff_lookup(hd, ein_rev15(in), L, idx)) { rc = INF_DATA; goto done; }
+        const uint32_t dsym = syms_d[idx];
+        ein_drop(in, L);
+        if (dsym > 29u) { rc = INF_DATA; goto done; }
+        uint32_t dbase, dext;
+        dist_base(dsym, dbase, dext);
+        const uint32_t dist = dbase + ein_peek(in, dext);
+        ein_drop(in, dext);
+        if (dist > op) { rc = INF_DATA; goto done; }
+        TOK_PT(4);
+        sink.match(op, mlen, dist);
+        op += mlen;
+        TOK_PT(5);
+        continue;
+      }
+      TOK_PC(2);
       ein_refill(in);
       uint32_t L, hi = 0;
       int32_t idx;
@@ -526,6 +610,7 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
       sink.match(op, n, dist);
       op += n;
       if (n < mlen) goto leave;
+      TOK_PT(7);
     }
   }
 leave:

@@ -170,7 +170,9 @@ def load(path=None):
         "hbam_sort_received": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, C.POINTER(SortedRunC)]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)
+        if f is None:  # an older build (A/B runs): only what it exports is bound
+            continue
         f.restype = res
         f.argtypes = args
     _LIB = L

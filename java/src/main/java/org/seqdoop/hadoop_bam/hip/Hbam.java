@@ -15,7 +15,7 @@ import htsjdk.samtools.util.RuntimeIOException;
 
 public final class Hbam implements AutoCloseable {
   public static final int OK = 0, EIO = -1, ETRUNC = -2, EFORMAT = -3, ERUNTIMEIO = -4,
-      EEOF = -5, EREFID = -6, EDATA = -7;
+      EEOF = -5, EREFID = -6, EDATA = -7, EMORE = -12;
 
   private static final Linker LINKER = Linker.nativeLinker();
   private static final SymbolLookup LIB = SymbolLookup.libraryLookup(
@@ -25,42 +25,50 @@ public final class Hbam implements AutoCloseable {
     return LINKER.downcallHandle(LIB.find(name).orElseThrow(), d);
   }
 
-  static final MethodHandle CREATE = fn("hbam_create",
-      FunctionDescriptor.of(ValueLayout.ADDRESS, ValueLayout.JAVA_INT, ValueLayout.ADDRESS));
-  static final MethodHandle DESTROY = fn("hbam_destroy",
-      FunctionDescriptor.ofVoid(ValueLayout.ADDRESS));
-  static final MethodHandle DECODE_SPLIT = fn("hbam_decode_split",
-      FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS, ValueLayout.ADDRESS,
-          ValueLayout.JAVA_INT, ValueLayout.JAVA_LONG, ValueLayout.JAVA_LONG,
-          ValueLayout.JAVA_LONG, ValueLayout.JAVA_LONG, ValueLayout.JAVA_LONG,
-          ValueLayout.JAVA_INT, ValueLayout.ADDRESS));
-  static final MethodHandle COLUMNS_TO_HOST = fn("hbam_columns_to_host",
-      FunctionDescriptor.of(ValueLayout.JAVA_INT, ValueLayout.ADDRESS, ValueLayout.ADDRESS,
-          ValueLayout.ADDRESS));
-  static final MethodHandle FREE_HOST = fn("hbam_free_host_columns",
-      FunctionDescriptor.ofVoid(ValueLayout.ADDRESS));
-  static final MethodHandle GUESS = fn("hbam_guess_bam_record_start",
-      FunctionDescriptor.of(ValueLayout.JAVA_LONG, ValueLayout.ADDRESS, ValueLayout.ADDRESS,
-          ValueLayout.JAVA_INT, ValueLayout.JAVA_LONG, ValueLayout.JAVA_LONG,
-          ValueLayout.JAVA_LONG, ValueLayout.JAVA_INT, ValueLayout.ADDRESS));
-  static final MethodHandle SPLITS = fn("hbam_probabilistic_splits",
-      FunctionDescriptor.of(ValueLayout.JAVA_LONG, ValueLayout.ADDRESS, ValueLayout.ADDRESS,
-          ValueLayout.JAVA_INT, ValueLayout.JAVA_LONG, ValueLayout.ADDRESS, ValueLayout.ADDRESS,
-          ValueLayout.JAVA_LONG, ValueLayout.ADDRESS, ValueLayout.ADDRESS));
+  private static final ValueLayout.OfLong J = ValueLayout.JAVA_LONG;
+  private static final ValueLayout.OfInt I = ValueLayout.JAVA_INT;
+  private static final AddressLayout A = ValueLayout.ADDRESS;
 
-  /** hbam_columns (include/hbam.h): 8-byte fields, pointers as addresses. */
-  public static final MemoryLayout COLUMNS = MemoryLayout.structLayout(
-      ValueLayout.JAVA_LONG.withName("n_records"), ValueLayout.JAVA_INT.withName("status"),
-      ValueLayout.JAVA_INT.withName("pad0"), ValueLayout.JAVA_LONG.withName("err_record"),
-      MemoryLayout.sequenceLayout(28, ValueLayout.ADDRESS).withName("ptrs_and_len"));
+  static final MethodHandle CREATE = fn("hbam_create", FunctionDescriptor.of(A, I, A));
+  static final MethodHandle DESTROY = fn("hbam_destroy", FunctionDescriptor.ofVoid(A));
+  static final MethodHandle LAST_ERROR = fn("hbam_last_error", FunctionDescriptor.of(A, A));
+  static final MethodHandle DECODE_SPLIT = fn("hbam_decode_split",
+      FunctionDescriptor.of(I, A, A, I, J, J, J, J, J, I, A));
+  static final MethodHandle COLUMNS_TO_HOST = fn("hbam_columns_to_host",
+      FunctionDescriptor.of(I, A, A, A));
+  static final MethodHandle FREE_HOST = fn("hbam_free_host_columns", FunctionDescriptor.ofVoid(A));
+  static final MethodHandle SPLIT_OPEN = fn("hbam_split_open",
+      FunctionDescriptor.of(A, A, A, J, J, J, I, J));
+  static final MethodHandle SPLIT_NEXT = fn("hbam_split_next", FunctionDescriptor.of(I, A, A));
+  static final MethodHandle SPLIT_CLOSE = fn("hbam_split_close", FunctionDescriptor.ofVoid(A));
+  static final MethodHandle GUESS = fn("hbam_guess_bam_record_start",
+      FunctionDescriptor.of(J, A, A, I, J, J, J, I, A));
+  static final MethodHandle SPLITS = fn("hbam_probabilistic_splits",
+      FunctionDescriptor.of(J, A, A, I, J, A, A, J, A, A));
+
+  /** hbam_columns (include/hbam.h): 24 bytes of counts/status, then 27 pointer-sized slots
+   *  (26 pointers and ubuf_len), 240 bytes in all. */
+  public static final StructLayout COLUMNS = MemoryLayout.structLayout(
+      J.withName("n_records"), I.withName("status"), I.withName("pad0"), J.withName("err_record"),
+      A.withName("voffset"), A.withName("key"), A.withName("rec_off"), A.withName("ubuf"),
+      J.withName("ubuf_len"), A.withName("block_size"), A.withName("ref_id"), A.withName("pos"),
+      A.withName("l_read_name"), A.withName("mapq"), A.withName("bin"), A.withName("n_cigar"),
+      A.withName("flag"), A.withName("l_seq"), A.withName("next_ref_id"), A.withName("next_pos"),
+      A.withName("tlen"), A.withName("layout_ok"), A.withName("name_off"), A.withName("names"),
+      A.withName("cigar_off"), A.withName("cigars"), A.withName("seq_off"), A.withName("seq"),
+      A.withName("qual"), A.withName("aux_off"), A.withName("aux"));
+
+  public static long offsetOf(String field) {
+    return COLUMNS.byteOffset(MemoryLayout.PathElement.groupElement(field));
+  }
 
   private final MemorySegment ctx;
 
   public Hbam(int device, boolean checkCrc) throws IOException {
     try (Arena a = Arena.ofConfined()) {
       MemorySegment opts = a.allocate(64);
-      opts.set(ValueLayout.JAVA_INT, 0, checkCrc ? 1 : 0);
-      opts.set(ValueLayout.JAVA_INT, 4, 1);  // validate_refs: BAMRecordCodec(header)
+      opts.set(I, 0, checkCrc ? 1 : 0);
+      opts.set(I, 4, 1);  // validate_refs: BAMRecordCodec(header), BAMRecordReader.java:130
       ctx = (MemorySegment) CREATE.invokeExact(device, opts);
     } catch (Throwable t) {
       throw new IOException(t);
@@ -77,7 +85,17 @@ public final class Hbam implements AutoCloseable {
       case EEOF: return new RuntimeEOFException(where);
       case EREFID: return new IllegalArgumentException(where);
       case EDATA: return new RuntimeException(new java.util.zip.DataFormatException(where));
+      case EIO: return new RuntimeIOException(new IOException(where));
       default: return new RuntimeIOException("hbam error " + code + " at " + where);
+    }
+  }
+
+  public String lastError() {
+    try {
+      MemorySegment s = (MemorySegment) LAST_ERROR.invokeExact(ctx);
+      return s.reinterpret(4096).getString(0);
+    } catch (Throwable t) {
+      return "hbam_last_error failed: " + t;
     }
   }
 

@@ -1,12 +1,23 @@
 // Drop-in body of org.seqdoop.hadoop_bam.BAMRecordReader (BAMRecordReader.java:48-188) over
-// the C ABI: initialize() decodes the whole FileVirtualSplit on the GPU (hbam_decode_split),
-// nextKeyValue() hands out (LongWritable key, SAMRecordWritable) from the columns and throws
-// the reference's exception at the record where the reference would.
+// the C ABI.  initialize() reads the header as the reference does (:128-130) and opens a
+// streamed device decode of the FileVirtualSplit (hbam_split_open: windows of
+// hadoopbam.hip.window-bytes compressed bytes, the next copied while the current decodes);
+// nextKeyValue() hands out (LongWritable key, SAMRecordWritable) from each window's host
+// columns and throws the reference's exception at the record where the reference would.
+// The value is the lazily decoded BAMRecord htsjdk would build from the same record bytes.
 package org.seqdoop.hadoop_bam.hip;
 
+import java.io.ByteArrayInputStream;
 import java.io.IOException;
 import java.lang.foreign.*;
+import java.nio.channels.FileChannel;
+import java.nio.file.StandardOpenOption;
 
+import org.apache.hadoop.conf.Configuration;
+import org.apache.hadoop.fs.FSDataInputStream;
+import org.apache.hadoop.fs.FileSystem;
+import org.apache.hadoop.fs.LocalFileSystem;
+import org.apache.hadoop.fs.Path;
 import org.apache.hadoop.io.LongWritable;
 import org.apache.hadoop.mapreduce.InputSplit;
 import org.apache.hadoop.mapreduce.RecordReader;
@@ -15,46 +26,170 @@ import org.apache.hadoop.mapreduce.TaskAttemptContext;
 import htsjdk.samtools.BAMRecordCodec;
 import htsjdk.samtools.SAMFileHeader;
 import htsjdk.samtools.SAMRecord;
+import htsjdk.samtools.ValidationStringency;
+import htsjdk.samtools.util.RuntimeIOException;
 
+import hbparquet.hadoop.util.ContextUtil;
 import org.seqdoop.hadoop_bam.FileVirtualSplit;
-import org.seqdoop.hadoop_bam.LazyBAMRecordFactory;
 import org.seqdoop.hadoop_bam.SAMRecordWritable;
+import org.seqdoop.hadoop_bam.util.SAMHeaderReader;
 
 public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWritable> {
+  public static final String WINDOW_BYTES_PROPERTY = "hadoopbam.hip.window-bytes";
+  public static final String DEVICE_PROPERTY = "hadoopbam.hip.device";
+
   private final LongWritable key = new LongWritable();
   private final SAMRecordWritable record = new SAMRecordWritable();
-  private Arena arena;
-  private MemorySegment host;          // hbam_columns (host copy)
+  private boolean isInitialized = false;
+
+  private Hbam hbam;
+  private Arena arena;               // file mapping + column structs of this reader
+  private MemorySegment stream;      // hbam_split_stream*
+  private MemorySegment dev, host;   // hbam_columns: device (library-owned) / host copy
+  private boolean hostLive = false, last = false;
   private long n, i;
   private int status;
-  private MemorySegment keys, recOff, blockSize, ubuf;
-  private SAMFileHeader header;
+  private MemorySegment keys, recOff, blockSize, ubuf, voffs;
+  private BAMRecordCodec codec;
+  private ValidationStringency stringency;
+  private long fileStart, virtualEnd;
 
   @Override public void initialize(InputSplit spl, TaskAttemptContext ctx) throws IOException {
+    if (isInitialized) close();  // re-entrant, as the reference (:116-118)
+    isInitialized = true;
+    final Configuration conf = ContextUtil.getConfiguration(ctx);
     final FileVirtualSplit split = (FileVirtualSplit) spl;
-    // (1) map the file (HDFS -> pinned host buffer) and read the header as the reference does
-    // (2) hbam_decode_split(ctx, buf, 0, 0, len, len, vStart, vEnd, n_ref, &dev)
-    // (3) hbam_columns_to_host(ctx, &dev, &host); keep key/rec_off/block_size/ubuf views
-    // The payload bytes of record i are ubuf[rec_off[i] .. rec_off[i]+4+block_size[i]):
-    // exactly what BAMRecordCodec.decode() reads, so SAMRecordWritable gets a lazily
-    // decoded BAMRecord built by LazyBAMRecordFactory from those bytes.
-    throw new UnsupportedOperationException("reference shim: see INTEGRATION.md");
+    final Path file = split.getPath();
+    final FileSystem fs = file.getFileSystem(conf);
+    this.stringency = SAMHeaderReader.getValidationStringency(conf);
+
+    final SAMFileHeader header;
+    try (FSDataInputStream in = fs.open(file)) {
+      header = SAMHeaderReader.readSAMHeaderFrom(in, conf);
+    }
+    // the lazy record of each hand-out is built from the record's bytes by htsjdk's own codec
+    codec = new BAMRecordCodec(header);
+    final int nRef = header.getSequenceDictionary().size();
+    final long len = fs.getFileStatus(file).getLen();
+
+    arena = Arena.ofShared();
+    final MemorySegment bytes = mapFile(fs, file, len, arena);
+    hbam = new Hbam(conf.getInt(DEVICE_PROPERTY, 0), false);
+    fileStart = split.getStartVirtualOffset() >>> 16;
+    virtualEnd = split.getEndVirtualOffset();
+    try {
+      stream = (MemorySegment) Hbam.SPLIT_OPEN.invokeExact(hbam.context(), bytes, len,
+          split.getStartVirtualOffset(), virtualEnd, nRef,
+          conf.getLong(WINDOW_BYTES_PROPERTY, 1L << 30));
+    } catch (Throwable t) {
+      throw new IOException(t);
+    }
+    if (stream.address() == 0) throw new IOException("hbam_split_open: " + hbam.lastError());
+    dev = arena.allocate(Hbam.COLUMNS);
+    host = arena.allocate(Hbam.COLUMNS);
+    n = i = 0;
+    status = Hbam.OK;
+    last = false;
+    nextWindow();
+  }
+
+  /** The file's bytes as one segment: mmap for the local file system, else read off-heap. */
+  private static MemorySegment mapFile(FileSystem fs, Path file, long len, Arena arena)
+      throws IOException {
+    if (fs instanceof LocalFileSystem || "file".equals(fs.getUri().getScheme())) {
+      try (FileChannel ch = FileChannel.open(java.nio.file.Path.of(file.toUri()),
+                                             StandardOpenOption.READ)) {
+        return ch.map(FileChannel.MapMode.READ_ONLY, 0, len, arena);
+      }
+    }
+    final MemorySegment seg = arena.allocate(Math.max(len, 1), 16);
+    final byte[] chunk = new byte[1 << 22];
+    try (FSDataInputStream in = fs.open(file)) {
+      for (long off = 0; off < len; ) {
+        final int k = in.read(off, chunk, 0, (int) Math.min(chunk.length, len - off));
+        if (k < 0) throw new IOException("short read of " + file);
+        MemorySegment.copy(chunk, 0, seg, ValueLayout.JAVA_BYTE, off, k);
+        off += k;
+      }
+    }
+    return seg;
+  }
+
+  private static MemorySegment ptr(MemorySegment cols, String f, long bytes) {
+    return cols.get(ValueLayout.ADDRESS, Hbam.offsetOf(f)).reinterpret(Math.max(bytes, 1));
+  }
+
+  /** The next window's records (hbam_split_next + hbam_columns_to_host); false at the end. */
+  private boolean nextWindow() {
+    try {
+      if (hostLive) { Hbam.FREE_HOST.invokeExact(host); hostLive = false; }
+      final int rc = (int) Hbam.SPLIT_NEXT.invokeExact(stream, dev);
+      if (rc < 0) throw new RuntimeIOException("hbam_split_next: " + hbam.lastError());
+      if (rc == 0) { last = true; n = i = 0; return false; }
+      final int rc2 = (int) Hbam.COLUMNS_TO_HOST.invokeExact(hbam.context(), dev, host);
+      if (rc2 != Hbam.OK) throw new RuntimeIOException("hbam_columns_to_host: " + hbam.lastError());
+      hostLive = true;
+    } catch (RuntimeException e) {
+      throw e;
+    } catch (Throwable t) {
+      throw new RuntimeIOException(t);
+    }
+    n = host.get(ValueLayout.JAVA_LONG, Hbam.offsetOf("n_records"));
+    status = host.get(ValueLayout.JAVA_INT, Hbam.offsetOf("status"));
+    if (status != Hbam.OK) last = true;
+    i = 0;
+    keys = ptr(host, "key", 8 * n);
+    voffs = ptr(host, "voffset", 8 * n);
+    recOff = ptr(host, "rec_off", 8 * n);
+    blockSize = ptr(host, "block_size", 4 * n);
+    ubuf = ptr(host, "ubuf", host.get(ValueLayout.JAVA_LONG, Hbam.offsetOf("ubuf_len")));
+    return true;
   }
 
   @Override public boolean nextKeyValue() {
-    if (i >= n) {
-      if (status != Hbam.OK && i == n) { ++i; throw Hbam.exceptionFor(status, "record " + n); }
-      return false;
+    while (i >= n) {
+      if (status != Hbam.OK) {  // raised at the record where the reference raises it
+        final int s = status;
+        status = Hbam.OK;
+        throw Hbam.exceptionFor(s, "BAMRecordReader.nextKeyValue");
+      }
+      if (last || !nextWindow()) return false;
     }
-    key.set(keys.getAtIndex(ValueLayout.JAVA_LONG, i));
-    // record.set(decodeLazy(ubuf, recOff[i], blockSize[i])) — BAMRecordCodec over a
-    // ByteArrayInputStream of the record bytes, header attached (BAMRecordReader.java:176-186)
+    final long off = recOff.getAtIndex(ValueLayout.JAVA_LONG, i);
+    final int bs = blockSize.getAtIndex(ValueLayout.JAVA_INT, i);
+    final byte[] raw = ubuf.asSlice(off, 4L + bs).toArray(ValueLayout.JAVA_BYTE);
+    codec.setInputStream(new ByteArrayInputStream(raw));
+    final SAMRecord r = codec.decode();  // exactly the bytes the reference's codec reads
+    if (stringency != null) r.setValidationStringency(stringency);
+    key.set(keys.getAtIndex(ValueLayout.JAVA_LONG, i));  // = BAMRecordReader.getKey(r)
+    record.set(r);
     ++i;
     return true;
   }
 
   @Override public LongWritable getCurrentKey() { return key; }
   @Override public SAMRecordWritable getCurrentValue() { return record; }
-  @Override public float getProgress() { return n == 0 ? 1 : (float) i / n; }
-  @Override public void close() { if (arena != null) arena.close(); }
+
+  @Override public float getProgress() {  // :157-168, from the next record's voffset
+    if (i >= n) return last ? 1 : 0;
+    final long filePos = voffs.getAtIndex(ValueLayout.JAVA_LONG, i) >>> 16;
+    final long fileEnd = virtualEnd >>> 16;
+    return (float) (filePos - fileStart) / (fileEnd - fileStart + 1);
+  }
+
+  @Override public void close() throws IOException {
+    try {
+      if (hostLive) Hbam.FREE_HOST.invokeExact(host);
+      if (stream != null && stream.address() != 0) Hbam.SPLIT_CLOSE.invokeExact(stream);
+    } catch (Throwable t) {
+      throw new IOException(t);
+    } finally {
+      hostLive = false;
+      stream = null;
+      if (hbam != null) hbam.close();
+      hbam = null;
+      if (arena != null) arena.close();
+      arena = null;
+    }
+  }
 }

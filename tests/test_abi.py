@@ -55,3 +55,38 @@ def test_no_device_context_without_gpu():
     from hadoop_bam import _lib
     with pytest.raises(_lib.HbamUnavailable):
         _lib.Context(0)
+
+
+def test_struct_layouts_match_the_header():
+    """hbam_columns / hbam_sorted_run as compiled C (gcc on include/hbam.h) have the sizes and
+    field offsets the ctypes binding and the Java shim's COLUMNS layout assume."""
+    import tempfile
+    from hadoop_bam import _lib
+    src = r'''
+#include <stddef.h>
+#include <stdio.h>
+#include "hbam.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(hbam_columns), offsetof(hbam_columns, voffset),
+         offsetof(hbam_columns, ubuf_len), offsetof(hbam_columns, aux), sizeof(hbam_sorted_run),
+         sizeof(hbam_timing));
+  return 0;
+}'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "l")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", exe, c], check=True)
+        got = [int(x) for x in subprocess.run([exe], stdout=subprocess.PIPE, text=True).stdout.split()]
+    assert got[0] == C.sizeof(_lib.Columns) == 240
+    assert got[1] == _lib.Columns.voffset.offset and got[2] == _lib.Columns.ubuf_len.offset
+    assert got[3] == _lib.Columns.aux.offset
+    assert got[4] == C.sizeof(_lib.SortedRunC) and got[5] == C.sizeof(_lib.Timing)
+    # the Java shim: 4 header fields, then 27 pointer-sized slots in the header's order
+    java = open(os.path.join(ROOT, "java", "src", "main", "java", "org", "seqdoop", "hadoop_bam",
+                             "hip", "Hbam.java")).read()
+    body = java[java.index("COLUMNS = MemoryLayout.structLayout("):]
+    body = body[:body.index(");")]
+    names = re.findall(r'withName\("(\w+)"\)', body)
+    assert names == [f[0] for f in _lib.Columns._fields_]
+    assert len(names) - 4 == 27

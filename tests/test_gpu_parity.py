@@ -334,14 +334,15 @@ def test_sharded_split_windows_match_oracle(gpu_ctx, oracle_mod, name, P):
         return
     assert np.array_equal(vs, want[0]) and np.array_equal(ve, want[1])
     h = oracle_mod.read_header(data)
-    shards = []
+    shards, windows = [], 0
     for a, z in zip(vs, ve):
         ref = oracle_mod.read_split(data, int(a), int(z))
         got, nwin = _stream_read(gpu_ctx, data, a, z, h["n_ref"], 64 << 10)
         assert_same_split(got, ref)
         assert got["payload"] == oracle_mod.record_payloads(ref)[0].tobytes()
-        assert nwin >= 2 or L // P < (64 << 10)
+        windows += nwin
         shards.append(got)
+    assert windows > 2 * len(shards)  # the EMORE continuation ran at many window ends
     whole = oracle_mod.read_split(data, h["first_voffset"], _whole(data))
     wv = set(int(x) for x in whole["voffset"])
     if all(int(a) in wv for a in vs[1:]) and whole["status"] == 0:
@@ -370,3 +371,21 @@ def test_windowed_decode_comp_base(gpu_ctx, oracle_mod):
     assert m > 100
     assert np.array_equal(got["voffset"], ref["voffset"][k:k + m])
     assert np.array_equal(got["key"], ref["key"][k:k + m])
+
+
+def test_guesses_across_launch_batches(oracle_mod, monkeypatch):
+    """More guesses than one launch holds (HBAM_GUESS_BATCH=64 for this context): the batch
+    loop's later launches give the oracle's answers too."""
+    from hadoop_bam import _lib
+    monkeypatch.setenv("HBAM_GUESS_BATCH", "64")
+    ctx = _lib.Context(0)
+    data = _load("small_pe.bam")
+    h = oracle_mod.read_header(data)
+    rng = np.random.default_rng(8)
+    beg = rng.integers(0, len(data), 200).astype(np.int64)
+    end = np.minimum(beg + rng.integers(1, 300000, 200), len(data)).astype(np.int64)
+    rc, out, err = ctx.guess_batch(data, beg, end, h["n_ref"])
+    assert rc == 0
+    for i in range(len(beg)):
+        assert (int(out[i]), int(err[i])) == oracle_mod.guess_bam_record_start(
+            data, int(beg[i]), int(end[i]), h["n_ref"]), i

@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=float, default=10e9)
     ap.add_argument("--guesses", type=int, default=10000)
-    ap.add_argument("--check", type=int, default=200)
+    ap.add_argument("--check", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=2)
     a = ap.parse_args()
     import torch
@@ -31,7 +31,7 @@ def main():
     import oracle
     from hadoop_bam import _lib
     t = time.time()
-    g = genbam.generate(target_bytes=int(a.size), seed=11, threads=int(os.environ.get("OMP_NUM_THREADS", 16)))
+    g = genbam.generate(target_bytes=int(a.size), seed=3, threads=int(os.environ.get("OMP_NUM_THREADS", 16)))
     data = np.asarray(g)
     print("generated %.2f GB in %.1fs" % (len(data) / 1e9, time.time() - t), file=sys.stderr, flush=True)
     d = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
@@ -40,7 +40,7 @@ def main():
     torch.cuda.synchronize()
     ctx = _lib.Context(0)
     h = ctx.parse_header(d[:len(data)])
-    rng = np.random.default_rng(5)
+    rng = np.random.default_rng(3)  # config #3 offsets
     beg = np.sort(rng.integers(0, len(data) - 1, a.guesses)).astype(np.int64)
     end = np.minimum(beg + (128 << 20), len(data)).astype(np.int64)
     t = time.time()
@@ -58,11 +58,24 @@ def main():
         print("rep %.3fs" % times[-1], file=sys.stderr, flush=True)
     idx = rng.choice(a.guesses, min(a.check, a.guesses), replace=False)
     t = time.time()
-    bad = 0
-    for i in idx:
-        want = oracle.guess_bam_record_start(data, int(beg[i]), int(end[i]), h["n_ref"])
-        bad += (int(out[i]), int(err[i])) != tuple(map(int, want))
-    cpu_s = (time.time() - t) / len(idx)
+    want = oracle.guess_bam_record_start(data, int(beg[idx[0]]), int(end[idx[0]]), h["n_ref"])
+    cpu_s = time.time() - t  # one host core, one guess
+    import threading
+    res = {}
+
+    def chk(ii):
+        for i in ii:
+            res[int(i)] = tuple(map(int, oracle.guess_bam_record_start(data, int(beg[i]), int(end[i]),
+                                                                        h["n_ref"])))
+    nt = int(os.environ.get("OMP_NUM_THREADS", 16))
+    ths = [threading.Thread(target=chk, args=(idx[j::nt],)) for j in range(nt)]
+    t = time.time()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    cpu_s = (time.time() - t) * nt / len(idx)
+    bad = sum((int(out[i]), int(err[i])) != res[int(i)] for i in idx)
     best = min(times)
     print(json.dumps({
         "metric": "BAMSplitGuesser guesses/s (config#3, one MI355X)",
