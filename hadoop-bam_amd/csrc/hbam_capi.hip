@@ -50,6 +50,7 @@ enum BufId {
   B_LENS,
   B_BITMAP,
   B_TAILS,
+  B_EDGE,
   B_INFST,
   B_CRC,
   B_ENTRY,
@@ -390,13 +391,16 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
                    const uint64_t* uoff, uint8_t* ubuf, int32_t* st, bool want_crc, uint32_t* crc) {
   uint8_t* lens;
   uint32_t *bitmap, *tails;
+  uint8_t* edges;
   int rc;
   if ((rc = ensure(c, B_LENS, nb * LENS_SLOT, &lens))) return rc;
   if ((rc = ensure(c, B_BITMAP, nb * BITMAP_WORDS, &bitmap))) return rc;
   if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
+  if ((rc = ensure(c, B_EDGE, 32 * nb + 32, &edges))) return rc;
   if (nb) {
     k_inflate_tokens<<<grid_for(nb, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
-        dcomp, blk, uoff, (uint32_t)nb, ubuf, lens, bitmap, tails, st);
+        dcomp, blk, uoff, (uint32_t)nb, ubuf, lens, bitmap, tails, edges, st);
+    k_edge_merge<<<grid_for(2 * nb, 256), 256, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, edges);
     HIPCHK(c, hipEventRecord(c->ev[11], c->stream));
     k_resolve<<<(uint32_t)nb, 64, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, bitmap, tails, st);
   }
@@ -1780,6 +1784,11 @@ extern "C" int hbam_resolve_tokens(hbam_ctx* c, uint8_t* io, uint32_t isize, con
 extern "C" int hbam_prof_attach(void* dev) {
   unsigned long long* p = (unsigned long long*)dev;
   return hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_prof), &p, sizeof p) == hipSuccess ? 0 : -1;
+}
+extern "C" int hbam_prof_attach_trace(void* dev, unsigned int idx) {
+  unsigned long long* p = (unsigned long long*)dev;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_gtrace_idx), &idx, sizeof idx) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_gtrace), &p, sizeof p) == hipSuccess ? 0 : -1;
 }
 extern "C" int hbam_prof_attach_guess(void* dev) {
   unsigned long long* p = (unsigned long long*)dev;

@@ -215,6 +215,20 @@ __device__ int32_t gc_read(GBcis& b, GStream& f, uint8_t* dst, int32_t len) {
 }
 // BAMRecordCodec.decode with the lazy factory: 1 record, 0 null, <0 exception
 __device__ int32_t gc_decode(GBcis& b, GStream& f) {
+  // whole record inside the current block: the reads below only advance cur_off
+  if (b.cur_len >= 0 && b.cur_len - b.cur_off >= 4) {
+    const uint8_t* q = b.cur + b.cur_off;
+    const int32_t bs = (int32_t)((uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 |
+                                 (uint32_t)q[3] << 24);
+    if (bs < 32) {
+      b.cur_off += 4;
+      return HBAM_EFORMAT;
+    }
+    if (b.cur_len - b.cur_off - 4 >= bs) {
+      b.cur_off += 4 + bs;
+      return 1;
+    }
+  }
   uint8_t t[4];
   int32_t rc = gc_read(b, f, t, 4);
   if (rc == HBAM_EEOF) return 0;
@@ -540,6 +554,35 @@ __device__ int32_t g_next_bam_wave(Guesser& g, uint64_t cpv, int32_t up, int32_t
   return g_next_bam(g, cpv, last, csize);  // == -1; buf / cursor as after the last test
 }
 
+// Record-chain memo of one candidate block cp0.  A candidate's verdict (the codec loop of
+// :171-192) is a pure function of where its chain starts: gb_seek(cp0|up) leaves the same
+// stream state for every up, and the loop's (b, prev) are still (0, cp0) at every record start
+// inside cp0.  So every record start x inside cp0 that a chain decoded leads to the same end
+// (rc, b) and the same final stream state; a later candidate, or a later chain, that reaches x
+// takes that end without re-decoding (decoded_any = true, since x decodes).  Near the window
+// end, where every chain runs out of bytes, this turns the quadratic candidate walk of
+// :159-208 linear.  An end whose block lives in the in-lane scratch is not memoised (the next
+// candidate's seek overwrites the scratch).
+constexpr int32_t GW_MEMO = 1024;  // record starts remembered per chain
+struct ChainMemo {
+  uint16_t* pos[2];  // LDS: ascending record starts of the remembered chain / the chain in flight
+  int32_t n, cur;    // remembered count, cursor of the chain in flight
+  int64_t s_fpos;    // stream state inside cp0 the remembered chain started from
+  int32_t s_last_len, s_cur_len;
+  const uint8_t* s_cur;
+  int32_t rc, b;     // the end every remembered start leads to
+  int64_t block_addr, fpos;
+  int32_t last_len, cur_len, cur_off;
+  const uint8_t* cur_p;
+};
+
+#ifdef HBAM_PROF
+__device__ unsigned long long* g_gprof = nullptr;   // 8 u64 per guess (tools/prof_regions.py)
+__device__ unsigned long long* g_gtrace = nullptr;  // guess g_gtrace_idx's candidates: [0] = count,
+                                                    // then 2 u64 each (tools/diag_guess.py);
+                                                    // its cache at [8193..]: 4 u64 per block
+__device__ unsigned int g_gtrace_idx = 0;
+#endif
 // guessNextBAMRecordStart :109-212, one wave
 #ifdef HBAM_PROF
 #define GP_T(i)                                          \
@@ -556,7 +599,8 @@ __device__ int32_t g_next_bam_wave(Guesser& g, uint64_t cpv, int32_t up, int32_t
 #define GP_C(i) (void)0
 #endif
 __device__ int64_t g_guess_wave(Guesser& g, const uint8_t* file, int64_t flen, int64_t beg, int64_t end,
-                                int32_t* err, int32_t* s_mag, uint32_t* s_nmag, uint32_t lane
+                                int32_t* err, int32_t* s_mag, uint32_t* s_nmag, uint16_t* s_memo,
+                                uint32_t lane
 #ifdef HBAM_PROF
                                 , uint64_t* gp
 #endif
@@ -605,6 +649,9 @@ __device__ int64_t g_guess_wave(Guesser& g, const uint8_t* file, int64_t flen, i
   gp[7] = listed ? nmag : 100000u;
 #endif
   GP_T(0);  // magic listing
+  ChainMemo mm;
+  mm.pos[0] = s_memo;
+  mm.pos[1] = s_memo + GW_MEMO;
   for (int32_t cp = 0;; ++cp) {
     int32_t ppos, psize;
     GP_C(4);
@@ -616,6 +663,7 @@ __device__ int64_t g_guess_wave(Guesser& g, const uint8_t* file, int64_t flen, i
     const uint64_t cpv = (uint64_t)(uint32_t)cp0 << 16;
     if (gb_seek(g.bz, g.in, cpv)) continue;  // catch (Throwable)
     GP_T(1);
+    mm.n = 0;
     for (int32_t up = 0;; ++up) {
       GP_C(5);
       const int32_t up0 = up = g_next_bam_wave(g, cpv, up, psize, lane);
@@ -626,15 +674,74 @@ __device__ int64_t g_guess_wave(Guesser& g, const uint8_t* file, int64_t flen, i
       int b = 0;
       int32_t prev = cp0;
       int32_t rc = 0;
+      int32_t nn = 0;  // starts of this chain inside cp0, into mm.pos[1]
+      bool memo_hit = false;
+      mm.cur = 0;
+      // same cp0 stream state as the remembered chain (the first seek into cp0 may reuse a block
+      // the previous candidate block's chain left behind, with the stream elsewhere)
+      const int64_t s_fpos = g.in.pos;
+      const int32_t s_last_len = g.bz.last_len, s_cur_len = g.bz.cur_len;
+      const uint8_t* s_cur = g.bz.cur;
+      const bool memo_ok = mm.n > 0 && mm.s_fpos == s_fpos && mm.s_last_len == s_last_len &&
+                           mm.s_cur_len == s_cur_len && mm.s_cur == s_cur;
       while (b < 3) {
+        if (b == 0 && memo_ok) {
+          const int32_t x = g.bz.cur_off;
+          while (mm.cur < mm.n && (int32_t)mm.pos[0][mm.cur] < x) ++mm.cur;
+          if (mm.cur < mm.n && (int32_t)mm.pos[0][mm.cur] == x) {
+            memo_hit = true;
+            break;
+          }
+        }
+        const int32_t x0 = g.bz.cur_off;
         rc = gc_decode(g.bz, g.in);
         GP_C(6);
         if (rc <= 0) break;
+        if (b == 0 && nn < GW_MEMO) mm.pos[1][nn++] = (uint16_t)x0;
         decoded_any = true;
         const int32_t cp2 = (int32_t)(gb_tell(g.bz) >> 16);
         if (cp2 != prev) { prev = cp2; ++b; }
       }
+      if (memo_hit) {  // this chain joins the remembered one: take its end
+        rc = mm.rc;
+        b = mm.b;
+        decoded_any = true;
+        g.bz.block_addr = mm.block_addr;
+        g.bz.last_len = mm.last_len;
+        g.bz.cur_len = mm.cur_len;
+        g.bz.cur_off = mm.cur_off;
+        g.bz.cur = mm.cur_p;
+        g.in.pos = mm.fpos;
+      } else if (nn > 0 && !(g.bz.cur == g.bz.scratch && g.bz.cur_len >= 0)) {
+        uint16_t* t = mm.pos[0];  // remember this chain instead
+        mm.pos[0] = mm.pos[1];
+        mm.pos[1] = t;
+        mm.n = nn;
+        mm.s_fpos = s_fpos;
+        mm.s_last_len = s_last_len;
+        mm.s_cur_len = s_cur_len;
+        mm.s_cur = s_cur;
+        mm.rc = rc;
+        mm.b = b;
+        mm.block_addr = g.bz.block_addr;
+        mm.last_len = g.bz.last_len;
+        mm.cur_len = g.bz.cur_len;
+        mm.cur_off = g.bz.cur_off;
+        mm.cur_p = g.bz.cur;
+        mm.fpos = g.in.pos;
+      }
       GP_T(3);
+#ifdef HBAM_PROF
+      if (g_gtrace && blockIdx.x == g_gtrace_idx && lane == 0) {
+        const unsigned long long k = g_gtrace[0];
+        if (k < 4096) {
+          g_gtrace[1 + 2 * k] = (unsigned long long)(uint32_t)cp0 << 32 | (uint32_t)up0;
+          g_gtrace[2 + 2 * k] = (unsigned long long)(uint32_t)rc << 32 | (uint32_t)b << 8 |
+                                (decoded_any ? 1u : 0u) | (memo_hit ? 2u : 0u);
+          g_gtrace[0] = k + 1;
+        }
+      }
+#endif
       if (rc < 0) {
         if (rc == HBAM_EFORMAT || rc == HBAM_ETRUNC || rc == HBAM_ERUNTIMEIO || rc == HBAM_EREFID)
           continue;
@@ -652,9 +759,6 @@ __device__ int64_t g_guess_wave(Guesser& g, const uint8_t* file, int64_t flen, i
   }
 }
 
-#ifdef HBAM_PROF
-__device__ unsigned long long* g_gprof = nullptr;  // 8 u64 per guess (tools/prof_guess.py)
-#endif
 __global__ __launch_bounds__(64) void k_guess_bam_wave(const uint8_t* __restrict__ file, int64_t flen,
                                                        const int64_t* __restrict__ beg,
                                                        const int64_t* __restrict__ end, uint32_t k,
@@ -676,6 +780,7 @@ __global__ __launch_bounds__(64) void k_guess_bam_wave(const uint8_t* __restrict
   __shared__ uint32_t T[256];
   __shared__ int32_t s_mag[GW_MAG];
   __shared__ uint32_t s_nmag;
+  __shared__ uint16_t s_memo[2 * GW_MEMO];
   crc_table_init(T);
   const uint32_t i = blockIdx.x, lane = threadIdx.x;
   if (i >= k) return;
@@ -702,15 +807,25 @@ __global__ __launch_bounds__(64) void k_guess_bam_wave(const uint8_t* __restrict
   g.bz.check_crc = 1;
   int32_t e;
 #ifdef HBAM_PROF
+  if (g_gtrace && i == g_gtrace_idx && lane == 0) {
+    unsigned long long* q = g_gtrace + 8193;
+    q[0] = g.bz.cache.n;
+    for (uint32_t j = 0; j < g.bz.cache.n && j < 512; ++j) {
+      q[1 + 4 * j] = g.bz.cache.pos[j];
+      q[2 + 4 * j] = (unsigned long long)g.bz.cache.blk[j].clen << 32 | g.bz.cache.blk[j].isize;
+      q[3 + 4 * j] = (unsigned long long)(uint32_t)g.bz.cache.st[j] << 32 | g.bz.cache.crc[j];
+      q[4 + 4 * j] = (unsigned long long)g.bz.cache.blk[j].crc << 32 | g.bz.cache.blk[j].pad;
+    }
+  }
   uint64_t gp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
-  const int64_t r = g_guess_wave(g, file, flen, beg[i], end[i], &e, s_mag, &s_nmag, lane, gp);
+  const int64_t r = g_guess_wave(g, file, flen, beg[i], end[i], &e, s_mag, &s_nmag, s_memo, lane, gp);
   if (g_gprof && lane == 0) {
     gp[0] = __builtin_amdgcn_s_memtime() - t0;  // slot 0: whole guess (listing folded in below)
     for (int q = 0; q < 8; ++q) g_gprof[8 * (uint64_t)i + q] = gp[q];
   }
 #else
-  const int64_t r = g_guess_wave(g, file, flen, beg[i], end[i], &e, s_mag, &s_nmag, lane);
+  const int64_t r = g_guess_wave(g, file, flen, beg[i], end[i], &e, s_mag, &s_nmag, s_memo, lane);
 #endif
   if (lane == 0) {
     out[i] = r;

@@ -155,6 +155,7 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
                                                                   uint8_t* __restrict__ lens_scratch,
                                                                   uint32_t* __restrict__ bitmap,
                                                                   uint32_t* __restrict__ tails,
+                                                                  uint8_t* __restrict__ edges,
                                                                   int32_t* __restrict__ status) {
   // 320 B of LDS per lane (u8 lit/len + distance symbols): 20 KiB per workgroup -> 8 per CU
   __shared__ uint8_t s_ll[INFLATE_WG * 288];
@@ -174,7 +175,8 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
     st = INF_DATA;  // Inflater.setInput with a negative length
   } else {
     TSink sink;
-    sink.init(ubuf, uoff[b], r.isize, bitmap + (uint64_t)b * BITMAP_WORDS, tails + 2 * (uint64_t)b);
+    sink.init(ubuf, uoff[b], r.isize, bitmap + (uint64_t)b * BITMAP_WORDS, tails + 2 * (uint64_t)b,
+              edges + 32 * (uint64_t)b);
 #ifdef HBAM_PROF
     uint64_t pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pc[4] = {0, 0, 0, 0};
 #endif
@@ -201,6 +203,34 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
     g_prof[32 * (uint64_t)b + 11] = produced;
   }
 #endif
+}
+
+// The partial first / last chunks of each block (TSink edge slots) -> this block's bytes of
+// them in ubuf.  One thread per (block, slot); neighbours write disjoint bytes of a shared
+// chunk.  Runs between the Huffman pass and k_resolve.
+__global__ void k_edge_merge(const BlockRec* __restrict__ blk, const uint64_t* __restrict__ uoff,
+                             uint32_t nblk, uint8_t* __restrict__ ubuf, const uint8_t* __restrict__ edges) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t b = (uint32_t)(i >> 1), slot = (uint32_t)(i & 1);
+  if (b >= nblk) return;
+  const uint32_t isize = blk[b].isize;
+  if (isize == 0 || isize > 65536u || blk[b].clen < 26u) return;  // no Huffman pass ran
+  const uint64_t start = uoff[b];
+  const uint32_t soff = (uint32_t)(start & 15u), iend = soff + isize;
+  uint8_t* base = ubuf + (start & ~15ull);
+  const uint8_t* src = edges + 32 * (uint64_t)b + 16u * slot;
+  uint32_t lo, hi;
+  if (slot == 0) {
+    if (soff == 0) return;
+    lo = soff;
+    hi = iend < 16u ? iend : 16u;
+  } else {
+    const uint32_t cl = (iend - 1u) >> 4;
+    if ((iend & 15u) == 0 || (cl == 0 && soff != 0)) return;
+    lo = cl << 4;
+    hi = iend;
+  }
+  for (uint32_t r = lo; r < hi; ++r) base[r] = src[r & 15u];
 }
 
 // LZ77 resolution of one block (phase 2 of the batched inflate); see resolve_dev.h.
@@ -243,7 +273,11 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
   const uint64_t abase = base & ~15ULL;
   const uint32_t a0 = (uint32_t)(base - abase);
   const uint64_t aend = base + isize;
-  const uint32_t nstr = (isize + RS_S - 1) / RS_S;
+  // Stretch k writes back global [abase + k*RS_S, +RS_S) = block offsets [k*RS_S - a0, ..): a
+  // block that does not start 16-aligned needs one more stretch than ISIZE alone when its
+  // last bytes fall past nstr*RS_S - a0 (the matches listed for stretch k, positions
+  // [k*RS_S, (k+1)*RS_S), reach a0 bytes into the next stretch's bytes).
+  const uint32_t nstr = (a0 + isize + RS_S - 1) / RS_S;
   // raw stretch k occupies global [abase + k*RS_S, +RS_S) (16-byte chunks, 2 per lane)
   auto load_raw = [&](uint32_t k, uint4& r0, uint4& r1) {
     const uint64_t g = abase + (uint64_t)k * RS_S + 16u * lane;

@@ -146,6 +146,77 @@ __device__ __forceinline__ uint32_t ein_rev15(const EIn& e) {
   return __builtin_bitreverse32((uint32_t)e.bb) >> 17;
 }
 
+// ---- packed canonical decode tables (symbol loop) ---------------------------------------
+// The lookup is the loop's largest VALU cost: 14 compares of the 15-bit code against the
+// per-length limits, each feeding a length count, an index offset and (lit/len) the symbol's
+// bit 8.  Pairs of limits in 16-bit halves let one v_pk_sub_u16 (clamp) + v_pk_min_u16 form
+// two compare results as 0/1 halves and v_pk_mad_u16 fold them into the offsets, about half
+// the instructions of the 32-bit chain.  Offsets are kept as 16-bit deltas: the sums are exact
+// mod 2^16 and every valid index is < 288.
+// (inline VOP3P: written as vector ops, LLVM splits the saturating subtract back into
+// per-half compares and selects)
+__device__ __forceinline__ uint32_t pk_sub_sat(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_pk_add_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk2(uint32_t lo, uint32_t hi) { return (lo & 0xffffu) | hi << 16; }
+struct HuffP {
+  uint32_t lim[7];  // (lim[2j], lim[2j+1]) as u16 halves
+  uint32_t dof[7];  // (doff[2j+1], doff[2j+2])
+  uint32_t dhl[7];  // lit/len: (hlim[2j+1] - hlim[2j], hlim[2j+2] - hlim[2j+1])
+  uint32_t lim14;   // v < lim14 <=> v starts a valid code
+  uint32_t o0;      // doff[0]
+  uint32_t t0;      // hlim[0]
+};
+__device__ __forceinline__ void huffp_make(const Huff& h, HuffP& p) {
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    p.lim[j] = pk2(h.lim[2 * j], h.lim[2 * j + 1]);
+    p.dof[j] = pk2((uint32_t)h.doff[2 * j + 1], (uint32_t)h.doff[2 * j + 2]);
+    p.dhl[j] = pk2(h.hlim[2 * j + 1] - h.hlim[2 * j], h.hlim[2 * j + 2] - h.hlim[2 * j + 1]);
+  }
+  p.lim14 = h.lim[14];
+  p.o0 = (uint32_t)h.doff[0];
+  p.t0 = h.hlim[0];
+}
+// code length / symbol index (/ bit 8 of a lit/len symbol) of a left-justified 15-bit value;
+// false: no code starts with v
+template <bool HI>
+__device__ __forceinline__ bool huffp_lookup(const HuffP& h, uint32_t v, uint32_t& L, uint32_t& idx,
+                                             uint32_t& hi) {
+  const uint32_t vv = (v + 1u) * 0x10001u;  // v + 1 <= 32768 in both halves
+  const uint32_t one = 0x10001u;
+  uint32_t sl = 0, so = 0, st = 0;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const uint32_t ge = pk_min(pk_sub_sat(vv, h.lim[j]), one);  // v >= lim, per half
+    sl = pk_add(sl, ge);
+    so = pk_mad(ge, h.dof[j], so);
+    if (HI) st = pk_mad(ge, h.dhl[j], st);
+  }
+  const uint32_t l = 1u + (sl & 0xffffu) + (sl >> 16);
+  L = l;
+  idx = (h.o0 + so + (so >> 16) + (v >> (15u - l))) & 0xffffu;
+  if (HI) hi = v >= ((h.t0 + st + (st >> 16)) & 0xffffu) ? 256u : 0u;
+  return v < h.lim14;
+}
+
 // ---- output ------------------------------------------------------------------------------
 struct TSink {
   uint8_t* cbase;   // 16-aligned address of chunk 0 (the chunk holding the block's first byte)
@@ -158,12 +229,14 @@ struct TSink {
   uint32_t nwin;    // windows covering the block
   uint32_t w0, w1, w2, w3;
   uint32_t* tail;   // [0] = op | n<<16 | 1<<31 for a final match shorter than 3 bytes, [1] = dist
+  uint8_t* edge;    // 32 B: the block's partial first / last 16-byte chunk (k_edge_merge)
 #ifdef HBAM_AB_NOSTORE
   uint64_t ab = 0;
 #endif
 
   __device__ __forceinline__ void init(uint8_t* ubuf, uint64_t start, uint32_t isize, uint32_t* bmp,
-                                       uint32_t* tl) {
+                                       uint32_t* tl, uint8_t* eg) {
+    edge = eg;
     cbase = ubuf + (start & ~15ull);
     soff = (uint32_t)(start & 15u);
     iend = soff + isize;
@@ -183,15 +256,13 @@ struct TSink {
     ab ^= lo ^ (hi << 1) ^ r0;  // A/B build only: output stores replaced by a register fold
     return;
 #endif
-    if (r0 >= soff && r0 + 16u <= iend) {
-      const uint4 v = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-      st_out((uint4*)(cbase + r0), v);
-    } else {  // chunk shared with a neighbouring block: only this block's bytes
-      for (uint32_t k = 0; k < 16u; ++k) {
-        const uint32_t r = r0 + k;
-        if (r >= soff && r < iend) cbase[r] = (uint8_t)((k < 8u ? lo >> (8u * k) : hi >> (8u * (k - 8u))) & 0xffu);
-      }
-    }
+    // A chunk shared with a neighbouring block (the block's first chunk when it does not
+    // start 16-aligned, its last when it does not end so) goes to the block's edge slot
+    // instead, whole; k_edge_merge writes this block's bytes of it afterwards.  So every flush
+    // is one 16-byte store and the loop carries no byte-store fallback.
+    const bool full = r0 >= soff && r0 + 16u <= iend;
+    uint8_t* dst = full ? cbase + r0 : edge + (r0 < soff ? 0u : 16u);
+    st_out((uint4*)dst, make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)));
   }
   __device__ __forceinline__ void chunk(uint32_t c) {
     if (c != curc) {
@@ -373,7 +444,7 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
   EIn in;
   ein_init(in, cdata, nbytes);
   uint32_t op = 0;
-  Huff hl, hd;
+  HuffP hl, hd;
   bool last = false;
   int32_t rc = INF_OK;
   uint32_t it = 0;  // iteration counter shared by the lanes of a phase (epoch clock)
@@ -416,9 +487,9 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
         for (int s = 0; s < 32; s += 4) d32[s / 4] = 0x05050505u;
         Huff t;
         tok_build(lens + TOK_LENS_LL, 288, syms_ll, t, 1);
-        hl = t;
+        huffp_make(t, hl);
         tok_build(lens + TOK_LENS_D, 32, syms_d, t, 2);
-        hd = t;
+        huffp_make(t, hd);
       } else if (type == 2u) {
         ein_ensure(in, 64);
         if (ein_avail(in) < 14u) goto leave;
@@ -499,9 +570,9 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
         {
           Huff t;
           if (!tok_build(lens + TOK_LENS_LL, (int)nlen, syms_ll, t, 1)) { rc = INF_DATA; goto done; }
-          hl = t;
+          huffp_make(t, hl);
           if (!tok_build(lens + TOK_LENS_D, (int)ndist, syms_d, t, 2)) { rc = INF_DATA; goto done; }
-          hd = t;
+          huffp_make(t, hd);
         }
       } else {
         rc = INF_DATA;  // invalid block type
@@ -516,38 +587,50 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
     TOK_PT(6);  // header + tables
     for (;;) {
       TOK_PC(0);
-      if ((++it & (TOK_K - 1u)) == 0u) ein_epoch(in);
-      if (ein_short(in, 48)) {
+      // epoch clock: the first active lane's, so the branch is scalar and every active lane
+      // merges / requests its quad at the same iteration
+      if ((__builtin_amdgcn_readfirstlane(++it) & (TOK_K - 1u)) == 0u) ein_epoch(in);
+      if (ein_short(in, 64)) {
         TOK_PC(1);
         TOK_PT(0);
         continue;  // stall until the next epoch merges more input
       }
       TOK_PT(0);
-      if (in.total - in.consumed >= 48u && op + 258u <= isize) {
-        // Fast path: at least one whole lit/len + distance's bits left in the stream and room
-        // for the longest match, so none of zlib's end-of-input / end-of-output outcomes can
-        // occur in this iteration and their checks are skipped.
+      if (in.total - in.consumed >= 64u) {
+        // Fast path: 64 stream bits left cover two lit/len codes + length extra + distance
+        // code + distance extra (15+15+5+15+13), so zlib's end-of-input outcomes cannot occur
+        // and after one refill (>= 33 bits in bb) none is checked.  A literal is followed by a
+        // second lit/len decode in the same iteration: the wave pays for the match path once
+        // per iteration either way, and most symbols are literals.
         ein_refill(in);
-        uint32_t L, hi = 0;
-        int32_t idx;
-        if (!huff_lookup_hi(hl, ein_rev15(in), L, idx, hi)) { rc = INF_DATA; goto done; }
-        const uint32_t sym = (uint32_t)syms_ll[idx] | hi;
+        uint32_t L, idx, hi = 0;
+        if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) { rc = INF_DATA; goto done; }
+        uint32_t sym = (uint32_t)syms_ll[idx] | hi;
         ein_drop(in, L);
-        TOK_PT(1);
         if (sym < 256u) {
+          if (op == isize) goto leave;
           sink.literal(op++, sym);
-          TOK_PT(2);
-          continue;
+          if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) { rc = INF_DATA; goto done; }
+          sym = (uint32_t)syms_ll[idx] | hi;
+          ein_drop(in, L);
+          if (sym < 256u) {
+            if (op == isize) goto leave;
+            sink.literal(op++, sym);
+            TOK_PT(2);
+            continue;
+          }
         }
+        TOK_PT(1);
         if (sym == 256u) break;
         if (sym > 285u) { rc = INF_DATA; goto done; }
         uint32_t lbase, lext;
         length_base(sym, lbase, lext);
+        ein_refill(in);
         const uint32_t mlen = lbase + ein_peek(in, lext);
         ein_drop(in, lext);
-        ein_refill(in);
         TOK_PT(3);
-        if (!huff_lookup(hd, ein_rev15(in), L, idx)) { rc = INF_DATA; goto done; }
+        uint32_t dh;
+        if (!huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh)) { rc = INF_DATA; goto done; }
         const uint32_t dsym = syms_d[idx];
         ein_drop(in, L);
         if (dsym > 29u) { rc = INF_DATA; goto done; }
@@ -555,19 +638,23 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
         dist_base(dsym, dbase, dext);
         const uint32_t dist = dbase + ein_peek(in, dext);
         ein_drop(in, dext);
+        if (op == isize) goto leave;
         if (dist > op) { rc = INF_DATA; goto done; }
         TOK_PT(4);
-        sink.match(op, mlen, dist);
-        op += mlen;
+        uint32_t n = isize - op;
+        n = mlen < n ? mlen : n;
+        sink.match(op, n, dist);
+        op += n;
+        if (n < mlen) goto leave;
         TOK_PT(5);
         continue;
       }
+      // careful path (the stream's last 64 bits): every zlib outcome checked per step
       TOK_PC(2);
       ein_refill(in);
-      uint32_t L, hi = 0;
-      int32_t idx;
+      uint32_t L, idx, hi = 0;
       const uint32_t v = ein_rev15(in);
-      const bool ok = huff_lookup_hi(hl, v, L, idx, hi);
+      const bool ok = huffp_lookup<true>(hl, v, L, idx, hi);
       if (!ok) {
         if (ein_avail(in) >= 1u) { rc = INF_DATA; goto done; }
         goto leave;
@@ -589,7 +676,8 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
       ein_drop(in, lext);
       ein_refill(in);
       const uint32_t vd = ein_rev15(in);
-      const bool okd = huff_lookup(hd, vd, L, idx);
+      uint32_t dh;
+      const bool okd = huffp_lookup<false>(hd, vd, L, idx, dh);
       if (!okd) {
         if (ein_avail(in) >= 1u) { rc = INF_DATA; goto done; }
         goto leave;

@@ -903,8 +903,14 @@ class BAMInputFormat:
         n, vs, ve = ctx.probabilistic_splits(data, beg, end)
         if n < 0:
             raise_for(int(n), ctx.last_error())
-        for a, b in zip(vs, ve):
-            out.append(FileVirtualSplit(path, int(a), int(b), ()))
+        # each virtual split carries the locations of the FileSplit whose guess opened it
+        # (:201-203): the guess for split j lands in [beg_j, end_j), so the owner is the last j
+        # with beg_j <= the start's compressed offset
+        owners = np.searchsorted(np.asarray(beg, np.int64),
+                                 (np.asarray(vs, np.uint64) >> np.uint64(16)).astype(np.int64),
+                                 side="right") - 1
+        for a, b, o in zip(vs, ve, owners):
+            out.append(FileVirtualSplit(path, int(a), int(b), splits[i + max(int(o), 0)].getLocations()))
         return j
 
     def isSplitable(self, job=None, path=None):

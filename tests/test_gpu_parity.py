@@ -39,6 +39,43 @@ def test_scan_and_inflate_bit_exact(gpu_ctx, oracle_mod, name):
     assert u.tobytes() == want
 
 
+def _bgzf_block(payload, level=6):
+    """One BGZF block (BSIZE/CRC/ISIZE as htsjdk writes them) holding `payload`."""
+    import struct
+    c = zlib.compressobj(level, zlib.DEFLATED, -15)
+    body = c.compress(payload) + c.flush()
+    hdr = b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" + \
+        struct.pack("<H", len(body) + 25)
+    return hdr + body + struct.pack("<II", zlib.crc32(payload), len(payload))
+
+
+@pytest.mark.parametrize("fname", ["guess_window_4197.bin", "guess_window_7433.bin"])
+def test_inflate_every_output_misalignment(gpu_ctx, fname):
+    """Blocks whose output starts at each of the 16 offsets of a 16-byte chunk, among them
+    ISIZE % 16 != 0 blocks that end in a match (the LZ77 pass must resolve and write back
+    the last bytes of a block that starts unaligned).  Windows of the config #3 file."""
+    import struct
+    w = np.fromfile(os.path.join(GOLDEN, fname), np.uint8).tobytes()
+    blocks, p = [], w.find(b"\x1f\x8b\x08\x04")
+    while p + 18 <= len(w) and w[p:p + 4] == b"\x1f\x8b\x08\x04":
+        bs = struct.unpack("<H", w[p + 16:p + 18])[0] + 1
+        if p + bs > len(w):
+            break
+        blocks.append((p, bs) + struct.unpack("<II", w[p + bs - 8:p + bs]))
+        p += bs
+    assert any(b[3] % 16 for b in blocks)
+    want = {b[0]: zlib.decompressobj(-15).decompress(w[b[0] + 18:b[0] + b[1] - 8]) for b in blocks}
+    for lead in range(16):
+        data = w + _bgzf_block(bytes(range(65, 65 + lead))) if lead else w
+        lst = ([(len(w), len(data) - len(w), zlib.crc32(bytes(range(65, 65 + lead))), lead)] if lead else []) + blocks
+        B = {"coff": np.array([b[0] for b in lst], np.uint64), "clen": np.array([b[1] for b in lst], np.uint32),
+             "crc": np.array([b[2] for b in lst], np.uint32), "isize": np.array([b[3] for b in lst], np.uint32)}
+        rc, u, off, st = gpu_ctx.inflate(np.frombuffer(data, np.uint8), B, check_crc=True)
+        assert rc == 0 and np.all(st == 0), (lead, st)
+        for j, b in enumerate(lst[1 if lead else 0:], start=1 if lead else 0):
+            assert u[int(off[j]):int(off[j + 1])].tobytes() == want[b[0]], (lead, j)
+
+
 @pytest.mark.parametrize("kw", [dict(level=0), dict(level=1), dict(level=9),
                                 dict(uniform_qual=1, level=6), dict(payload=64, level=6),
                                 dict(payload=300, level=1, straddle=0)])
@@ -125,6 +162,24 @@ def test_guesses_random_offsets(gpu_ctx, oracle_mod):
         assert (int(out[i]), int(err[i])) == (g, e), i
 
 
+@pytest.mark.parametrize("level,k", [(0, 60), (1, 200)])
+def test_guesses_window_exhaustion(gpu_ctx, oracle_mod, genbam, level, k):
+    """Stored / barely compressed blocks: three block changes do not fit the 256 KiB guess
+    window, so every candidate's record chain runs out of bytes and the guesser walks the
+    record starts of the block one by one (BAMSplitGuesser.java:159-208) — the chain memo's
+    case.  Every guess equals the oracle's."""
+    data = np.asarray(genbam.generate(target_bytes=6 << 20, seed=11, level=level, threads=8))
+    h = oracle_mod.read_header(data)
+    rng = np.random.default_rng(5)
+    beg = np.sort(rng.integers(0, len(data), k)).astype(np.int64)
+    end = np.minimum(beg + (128 << 20), len(data)).astype(np.int64)
+    rc, out, err = gpu_ctx.guess_batch(data, beg, end, h["n_ref"])
+    assert rc == 0
+    for i in range(len(beg)):
+        g, e = oracle_mod.guess_bam_record_start(data, int(beg[i]), int(end[i]), h["n_ref"])
+        assert (int(out[i]), int(err[i])) == (g, e), i
+
+
 def test_bgzf_guesser(gpu_ctx, oracle_mod):
     data = _load("edge_uniform_long.bam")
     rng = np.random.default_rng(4)
@@ -193,7 +248,15 @@ def test_bam_input_format_record_reader(oracle_mod, tmp_path):
     path = os.path.join(GOLDEN, "small_pe.bam")
     data = _load("small_pe.bam")
     fmt = BAMInputFormat()
-    splits = fmt.getSplits(compute_file_splits(path, len(data), 512 << 10), Configuration())
+    fsplits = compute_file_splits(path, len(data), 512 << 10)
+    for j, f in enumerate(fsplits):
+        f.hosts = ["host%d" % j]
+    splits = fmt.getSplits(fsplits, Configuration())
+    # locations follow the FileSplit whose guess opened each virtual split (BAMInputFormat.java:202)
+    starts = [f.getStart() for f in fsplits]
+    for s in splits:
+        owner = max(j for j, b in enumerate(starts) if b <= s.getStartVirtualOffset() >> 16)
+        assert s.getLocations() == ["host%d" % owner]
     keys = []
     for s in splits:
         rr = fmt.createRecordReader(s, Configuration())

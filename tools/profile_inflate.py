@@ -32,7 +32,7 @@ if a.prof:
     import ctypes as C
     L = _lib.load()
     L.hbam_prof_attach.argtypes = [C.c_void_p]
-    pbuf = torch.zeros((len(data) // 8000 + 4096) * 16, dtype=torch.int64, device="cuda")
+    pbuf = torch.zeros((len(data) // 8000 + 4096) * 32, dtype=torch.int64, device="cuda")
     assert L.hbam_prof_attach(C.c_void_p(pbuf.data_ptr())) == 0
 h = ctx.parse_header(d[:len(data)])
 for _ in range(a.reps):
@@ -43,7 +43,7 @@ for _ in range(a.reps):
 
 if a.prof:
     nb = ctx.timing()["n_blocks"]
-    P = pbuf.view(-1, 16)[:nb].cpu().numpy().astype(np.float64)
+    P = pbuf.view(-1, 32)[:nb].cpu().numpy().astype(np.float64)
 
     def stats(name, col):
         v = P[:, col]
