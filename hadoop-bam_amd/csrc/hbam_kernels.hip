@@ -244,12 +244,15 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
   __shared__ uint64_t s_rec[RS_MAXM];   // pre matches from the front, ordered from the back
   __shared__ uint16_t s_pos[RS_MAXM];
   __shared__ uint64_t s_sel[8];
+#ifndef HBAM_RS_PREFIX
+  __shared__ uint32_t s_pend[RS_PW];
+#endif
   const uint32_t b = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   if (b >= nblk) return;
 #ifdef HBAM_PROF
   const uint64_t pr0 = PROF_RT(), pc0 = PROF_CLK();
-  uint64_t p_desc = 0, p_bat = 0, n_bat = 0, n_m = 0, p_st = 0;
+  uint64_t p_desc = 0, p_bat = 0, n_bat = 0, n_m = 0, p_st = 0, p_pre = 0, p_wb = 0;
 #endif
   if (status[b] != INF_OK) return;
   const uint32_t isize = blk[b].isize;
@@ -372,6 +375,62 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
       if (src + RS_W >= s0) rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
       else rs_copy_glb(s_buf, lbase + p, len, ubuf + base + src);
     }
+#ifdef HBAM_PROF
+    p_pre += PROF_CLK() - q1;
+#endif
+#ifndef HBAM_RS_PREFIX
+    // ---- ordered matches: dataflow rounds.  s_pend holds one bit per byte of the stretch
+    // (+ match spill) that an ordered match has yet to write; a match is ready when no byte of
+    // its external source [p - dist, p - dist + min(len, dist)) is pending.  Every round
+    // copies all ready matches at once and clears their bits, so the rounds are the depth of
+    // the stretch's match dependency graph (the earliest pending match is always ready).
+    if (nord) {
+      for (uint32_t w = lane; w < RS_PW; w += 64) s_pend[w] = 0u;
+      rs_wave_sync();
+      // this lane's matches lane + 64 t (s_rec, read back each round: registers for six
+      // slots would cost the kernel half its occupancy)
+      const uint32_t mine = nord > lane ? (nord - lane + 63u) / 64u : 0u;
+      uint32_t live = mine >= 32u ? ~0u : (1u << mine) - 1u;
+#pragma unroll 1
+      for (uint32_t t = 0; t < mine; ++t) {
+        const uint64_t rec = s_rec[RS_MAXM - 1 - (lane + 64u * t)];
+        rs_bits(s_pend, ((uint32_t)rec & 0xffffu) - s0, (uint32_t)(rec >> 16) & 0xffffu, true);
+      }
+      rs_wave_sync();
+      for (;;) {
+        uint32_t ready = 0;
+#pragma unroll 1
+        for (uint32_t t = 0; t < mine; ++t) {
+          if (!(live >> t & 1u)) continue;
+          const uint64_t rec = s_rec[RS_MAXM - 1 - (lane + 64u * t)];
+          const uint32_t p = (uint32_t)rec & 0xffffu, dist = (uint32_t)(rec >> 32) & 0xffffu;
+          const uint32_t e = (uint32_t)(rec >> 48);
+          const uint32_t a = p - dist;
+          const uint32_t lo = a > s0 ? a - s0 : 0u;  // bytes before the stretch are final
+          if (e <= s0 + lo || !rs_any_bit(s_pend, lo, e - s0)) ready |= 1u << t;
+        }
+#pragma unroll 1
+        for (uint32_t t = 0; t < mine; ++t) {
+          if (!(ready >> t & 1u)) continue;
+          const uint64_t rec = s_rec[RS_MAXM - 1 - (lane + 64u * t)];
+          const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
+                         dist = (uint32_t)(rec >> 32) & 0xffffu;
+          rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
+          rs_bits(s_pend, p - s0, len, false);
+        }
+        live &= ~ready;
+#ifdef HBAM_PROF
+        ++n_bat;
+#endif
+        if (!__any(live != 0u)) break;
+        if (!__any(ready != 0u)) {  // validated descriptors always make progress: corrupt
+          if (lane == 0) status[b] = INF_DATA;
+          return;
+        }
+        rs_wave_sync();
+      }
+    }
+#else
     // ---- ordered matches: in-order batches
     for (uint32_t kk = 0; kk < nord;) {
       const uint32_t j = kk + lane;
@@ -394,6 +453,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
       ++n_bat;
 #endif
     }
+#endif
     if ((tail0 & 0x80000000u) && (tail0 & 0xffffu) / RS_S == k && lane == 0) {
       // final match shorter than 3 bytes (the output filled up inside it); last token
       const uint32_t p = tail0 & 0xffffu, n = (tail0 >> 16) & 0x7fffu;
@@ -412,7 +472,8 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     }
     __syncthreads();
 #ifdef HBAM_PROF
-    p_bat += PROF_CLK() - q1;
+    const uint64_t q2 = PROF_CLK();
+    p_bat += q2 - q1;
 #endif
     // ---- write back stretch k (LDS [RS_W, RS_W + RS_S)), then slide the window by RS_S
     // (each lane moves its own 16-byte columns, so no barrier is needed inside the move)
@@ -438,6 +499,9 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = ra1;
     load_raw(k + 3, ra0, ra1);
     __syncthreads();
+#ifdef HBAM_PROF
+    p_wb += PROF_CLK() - q2;
+#endif
   }
 #ifdef HBAM_PROF
   if (g_prof && lane == 0) {
@@ -448,6 +512,8 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     g[3] = p_st;
     g[4] = p_desc;
     g[5] = p_bat;
+    g[12] = p_pre;
+    g[13] = p_wb;
     g[6] = n_bat;
     g[7] = n_m;
   }

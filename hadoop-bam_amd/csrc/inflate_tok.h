@@ -153,28 +153,10 @@ __device__ __forceinline__ uint32_t ein_rev15(const EIn& e) {
 // two compare results as 0/1 halves and v_pk_mad_u16 fold them into the offsets, about half
 // the instructions of the 32-bit chain.  Offsets are kept as 16-bit deltas: the sums are exact
 // mod 2^16 and every valid index is < 288.
-// (inline VOP3P: written as vector ops, LLVM splits the saturating subtract back into
-// per-half compares and selects)
-__device__ __forceinline__ uint32_t pk_sub_sat(uint32_t a, uint32_t b) {
-  uint32_t d;
-  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(d) : "v"(a), "v"(b));
-  return d;
-}
-__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
-  uint32_t d;
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
-  return d;
-}
-__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
-  uint32_t d;
-  asm("v_pk_add_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
-  return d;
-}
-__device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t d;
-  asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 __device__ __forceinline__ uint32_t pk2(uint32_t lo, uint32_t hi) { return (lo & 0xffffu) | hi << 16; }
 struct HuffP {
   uint32_t lim[7];  // (lim[2j], lim[2j+1]) as u16 halves
@@ -197,18 +179,52 @@ __device__ __forceinline__ void huffp_make(const Huff& h, HuffP& p) {
 }
 // code length / symbol index (/ bit 8 of a lit/len symbol) of a left-justified 15-bit value;
 // false: no code starts with v
+// Per pair j (inline VOP3P, one asm statement per group of pairs: written as vector C, LLVM
+// turns min(sub_sat) back into per-half compares and selects, and separate asm statements
+// each cost a hazard s_nop):
+//   g  = min(sat(v+1 - lim_j), 1)   the two "v >= lim" bits as 0/1 halves
+//   sl += g;  so += g * dof_j;  st += g * dhl_j
+#define HBAM_PK_PAIR(LIM, DOF, DHL)                 \
+  "v_pk_sub_u16 %[g], %[vv], " LIM " clamp\n\t"     \
+  "v_pk_min_u16 %[g], %[g], %[one]\n\t"              \
+  "v_pk_add_u16 %[sl], %[sl], %[g]\n\t"              \
+  "v_pk_mad_u16 %[so], %[g], " DOF ", %[so]\n\t"     \
+  "v_pk_mad_u16 %[st], %[g], " DHL ", %[st]\n\t"
+#define HBAM_PK_PAIR_NT(LIM, DOF)                   \
+  "v_pk_sub_u16 %[g], %[vv], " LIM " clamp\n\t"     \
+  "v_pk_min_u16 %[g], %[g], %[one]\n\t"              \
+  "v_pk_add_u16 %[sl], %[sl], %[g]\n\t"              \
+  "v_pk_mad_u16 %[so], %[g], " DOF ", %[so]\n\t"
 template <bool HI>
 __device__ __forceinline__ bool huffp_lookup(const HuffP& h, uint32_t v, uint32_t& L, uint32_t& idx,
                                              uint32_t& hi) {
   const uint32_t vv = (v + 1u) * 0x10001u;  // v + 1 <= 32768 in both halves
   const uint32_t one = 0x10001u;
-  uint32_t sl = 0, so = 0, st = 0;
-#pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const uint32_t ge = pk_min(pk_sub_sat(vv, h.lim[j]), one);  // v >= lim, per half
-    sl = pk_add(sl, ge);
-    so = pk_mad(ge, h.dof[j], so);
-    if (HI) st = pk_mad(ge, h.dhl[j], st);
+  uint32_t sl = 0, so = 0, st = 0, g;
+  if (HI) {
+    asm(HBAM_PK_PAIR("%[l0]", "%[d0]", "%[t0]") HBAM_PK_PAIR("%[l1]", "%[d1]", "%[t1]")
+        HBAM_PK_PAIR("%[l2]", "%[d2]", "%[t2]") HBAM_PK_PAIR("%[l3]", "%[d3]", "%[t3]")
+        : [sl] "+v"(sl), [so] "+v"(so), [st] "+v"(st), [g] "=&v"(g)
+        : [vv] "v"(vv), [one] "v"(one), [l0] "v"(h.lim[0]), [l1] "v"(h.lim[1]), [l2] "v"(h.lim[2]),
+          [l3] "v"(h.lim[3]), [d0] "v"(h.dof[0]), [d1] "v"(h.dof[1]), [d2] "v"(h.dof[2]),
+          [d3] "v"(h.dof[3]), [t0] "v"(h.dhl[0]), [t1] "v"(h.dhl[1]), [t2] "v"(h.dhl[2]),
+          [t3] "v"(h.dhl[3]));
+    asm(HBAM_PK_PAIR("%[l4]", "%[d4]", "%[t4]") HBAM_PK_PAIR("%[l5]", "%[d5]", "%[t5]")
+        HBAM_PK_PAIR("%[l6]", "%[d6]", "%[t6]")
+        : [sl] "+v"(sl), [so] "+v"(so), [st] "+v"(st), [g] "=&v"(g)
+        : [vv] "v"(vv), [one] "v"(one), [l4] "v"(h.lim[4]), [l5] "v"(h.lim[5]), [l6] "v"(h.lim[6]),
+          [d4] "v"(h.dof[4]), [d5] "v"(h.dof[5]), [d6] "v"(h.dof[6]), [t4] "v"(h.dhl[4]),
+          [t5] "v"(h.dhl[5]), [t6] "v"(h.dhl[6]));
+  } else {
+    asm(HBAM_PK_PAIR_NT("%[l0]", "%[d0]") HBAM_PK_PAIR_NT("%[l1]", "%[d1]")
+        HBAM_PK_PAIR_NT("%[l2]", "%[d2]") HBAM_PK_PAIR_NT("%[l3]", "%[d3]")
+        HBAM_PK_PAIR_NT("%[l4]", "%[d4]") HBAM_PK_PAIR_NT("%[l5]", "%[d5]")
+        HBAM_PK_PAIR_NT("%[l6]", "%[d6]")
+        : [sl] "+v"(sl), [so] "+v"(so), [g] "=&v"(g)
+        : [vv] "v"(vv), [one] "v"(one), [l0] "v"(h.lim[0]), [l1] "v"(h.lim[1]), [l2] "v"(h.lim[2]),
+          [l3] "v"(h.lim[3]), [l4] "v"(h.lim[4]), [l5] "v"(h.lim[5]), [l6] "v"(h.lim[6]),
+          [d0] "v"(h.dof[0]), [d1] "v"(h.dof[1]), [d2] "v"(h.dof[2]), [d3] "v"(h.dof[3]),
+          [d4] "v"(h.dof[4]), [d5] "v"(h.dof[5]), [d6] "v"(h.dof[6]));
   }
   const uint32_t l = 1u + (sl & 0xffffu) + (sl >> 16);
   L = l;
@@ -427,6 +443,101 @@ __device__ __attribute__((noinline)) bool tok_build(const uint8_t* __restrict__ 
   return true;
 }
 
+// One iteration of the symbol loop with >= 64 stream bits left: two lit/len codes + length
+// extra + distance code + distance extra (15+15+5+15+13) fit, so zlib's end-of-input outcomes
+// cannot occur and after one refill (>= 33 bits in bb) none is checked.  A literal is
+// followed by a second lit/len decode in the same iteration: the wave pays for the match path
+// once per iteration either way, and most symbols are literals.
+// Returns 0 next, 1 end of block, 2 output full (zlib stops), 3 data error.
+__device__ __forceinline__ uint32_t tok_fast(EIn& in, const HuffP& hl, const HuffP& hd,
+                                             const uint8_t* __restrict__ syms_ll,
+                                             const uint8_t* __restrict__ syms_d, TSink& sink,
+                                             uint32_t& op, uint32_t isize) {
+  ein_refill(in);
+  uint32_t L, idx, hi = 0;
+  if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) return 3u;
+  uint32_t sym = (uint32_t)syms_ll[idx] | hi;
+  ein_drop(in, L);
+  if (sym < 256u) {
+    if (op == isize) return 2u;
+    sink.literal(op++, sym);
+    if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) return 3u;
+    sym = (uint32_t)syms_ll[idx] | hi;
+    ein_drop(in, L);
+    if (sym < 256u) {
+      if (op == isize) return 2u;
+      sink.literal(op++, sym);
+      return 0u;
+    }
+  }
+  if (sym == 256u) return 1u;
+  if (sym > 285u) return 3u;
+  uint32_t lbase, lext;
+  length_base(sym, lbase, lext);
+  ein_refill(in);
+  const uint32_t mlen = lbase + ein_peek(in, lext);
+  ein_drop(in, lext);
+  uint32_t dh;
+  if (!huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh)) return 3u;
+  const uint32_t dsym = syms_d[idx];
+  ein_drop(in, L);
+  if (dsym > 29u) return 3u;
+  uint32_t dbase, dext;
+  dist_base(dsym, dbase, dext);
+  const uint32_t dist = dbase + ein_peek(in, dext);
+  ein_drop(in, dext);
+  if (op == isize) return 2u;
+  if (dist > op) return 3u;
+  uint32_t n = isize - op;
+  n = mlen < n ? mlen : n;
+  sink.match(op, n, dist);
+  op += n;
+  return n < mlen ? 2u : 0u;
+}
+// One symbol with every zlib outcome checked (the stream's last 64 bits).
+__device__ __forceinline__ uint32_t tok_careful(EIn& in, const HuffP& hl, const HuffP& hd,
+                                                const uint8_t* __restrict__ syms_ll,
+                                                const uint8_t* __restrict__ syms_d, TSink& sink,
+                                                uint32_t& op, uint32_t isize) {
+  ein_refill(in);
+  uint32_t L, idx, hi = 0;
+  if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) return ein_avail(in) >= 1u ? 3u : 2u;
+  if (L > ein_avail(in)) return 2u;
+  const uint32_t sym = (uint32_t)syms_ll[idx] | hi;
+  ein_drop(in, L);
+  if (sym < 256u) {
+    if (op == isize) return 2u;
+    sink.literal(op++, sym);
+    return 0u;
+  }
+  if (sym == 256u) return 1u;
+  if (sym > 285u) return 3u;
+  uint32_t lbase, lext;
+  length_base(sym, lbase, lext);
+  if (lext > ein_avail(in)) return 2u;
+  const uint32_t mlen = lbase + ein_peek(in, lext);
+  ein_drop(in, lext);
+  ein_refill(in);
+  uint32_t dh;
+  if (!huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh)) return ein_avail(in) >= 1u ? 3u : 2u;
+  if (L > ein_avail(in)) return 2u;
+  const uint32_t dsym = syms_d[idx];
+  ein_drop(in, L);
+  if (dsym > 29u) return 3u;
+  uint32_t dbase, dext;
+  dist_base(dsym, dbase, dext);
+  if (dext > ein_avail(in)) return 2u;
+  const uint32_t dist = dbase + ein_peek(in, dext);
+  ein_drop(in, dext);
+  if (op == isize) return 2u;
+  if (dist > op) return 3u;
+  uint32_t n = isize - op;
+  n = mlen < n ? mlen : n;
+  sink.match(op, n, dist);
+  op += n;
+  return n < mlen ? 2u : 0u;
+}
+
 // Inflate one raw DEFLATE stream (cdata, nbytes) to exactly isize bytes into the token sink.
 // syms_ll: 288 u8 LDS slots (symbol & 255; bit 8 from Huff.hlim); syms_d: 32 u8 LDS slots;
 // lens: LENS_SLOT bytes of 16-aligned global scratch.  Returns INF_OK / INF_SHORT / INF_DATA.
@@ -584,121 +695,31 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
     // the iteration's own output stores.
     __builtin_amdgcn_s_waitcnt(0);
     // ---- symbols of a Huffman-coded block
+    // One structured loop (no continue / goto inside): every path of an iteration joins at
+    // the loop's end with an exit code, so the decoder state needs no per-path copies.
     TOK_PT(6);  // header + tables
-    for (;;) {
-      TOK_PC(0);
-      // epoch clock: the first active lane's, so the branch is scalar and every active lane
-      // merges / requests its quad at the same iteration
-      if ((__builtin_amdgcn_readfirstlane(++it) & (TOK_K - 1u)) == 0u) ein_epoch(in);
-      if (ein_short(in, 64)) {
-        TOK_PC(1);
-        TOK_PT(0);
-        continue;  // stall until the next epoch merges more input
-      }
-      TOK_PT(0);
-      if (in.total - in.consumed >= 64u) {
-        // Fast path: 64 stream bits left cover two lit/len codes + length extra + distance
-        // code + distance extra (15+15+5+15+13), so zlib's end-of-input outcomes cannot occur
-        // and after one refill (>= 33 bits in bb) none is checked.  A literal is followed by a
-        // second lit/len decode in the same iteration: the wave pays for the match path once
-        // per iteration either way, and most symbols are literals.
-        ein_refill(in);
-        uint32_t L, idx, hi = 0;
-        if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) { rc = INF_DATA; goto done; }
-        uint32_t sym = (uint32_t)syms_ll[idx] | hi;
-        ein_drop(in, L);
-        if (sym < 256u) {
-          if (op == isize) goto leave;
-          sink.literal(op++, sym);
-          if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) { rc = INF_DATA; goto done; }
-          sym = (uint32_t)syms_ll[idx] | hi;
-          ein_drop(in, L);
-          if (sym < 256u) {
-            if (op == isize) goto leave;
-            sink.literal(op++, sym);
-            TOK_PT(2);
-            continue;
-          }
+    {
+      uint32_t ex = 0;  // 0 next symbol, 1 end of block, 2 leave (zlib stops), 3 data error
+      do {
+        TOK_PC(0);
+        // epoch clock: the first active lane's, so the branch is scalar and every active lane
+        // merges / requests its quad at the same iteration
+        if ((__builtin_amdgcn_readfirstlane(++it) & (TOK_K - 1u)) == 0u) ein_epoch(in);
+        if (!ein_short(in, 64)) {  // else stall until the next epoch merges more input
+          if (in.total - in.consumed >= 64u)
+            ex = tok_fast(in, hl, hd, syms_ll, syms_d, sink, op, isize);
+          else
+            ex = tok_careful(in, hl, hd, syms_ll, syms_d, sink, op, isize);
         }
+#ifdef HBAM_PROF
         TOK_PT(1);
-        if (sym == 256u) break;
-        if (sym > 285u) { rc = INF_DATA; goto done; }
-        uint32_t lbase, lext;
-        length_base(sym, lbase, lext);
-        ein_refill(in);
-        const uint32_t mlen = lbase + ein_peek(in, lext);
-        ein_drop(in, lext);
-        TOK_PT(3);
-        uint32_t dh;
-        if (!huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh)) { rc = INF_DATA; goto done; }
-        const uint32_t dsym = syms_d[idx];
-        ein_drop(in, L);
-        if (dsym > 29u) { rc = INF_DATA; goto done; }
-        uint32_t dbase, dext;
-        dist_base(dsym, dbase, dext);
-        const uint32_t dist = dbase + ein_peek(in, dext);
-        ein_drop(in, dext);
-        if (op == isize) goto leave;
-        if (dist > op) { rc = INF_DATA; goto done; }
-        TOK_PT(4);
-        uint32_t n = isize - op;
-        n = mlen < n ? mlen : n;
-        sink.match(op, n, dist);
-        op += n;
-        if (n < mlen) goto leave;
-        TOK_PT(5);
-        continue;
+#endif
+      } while (ex == 0u);
+      if (ex == 2u) goto leave;
+      if (ex == 3u) {
+        rc = INF_DATA;
+        goto done;
       }
-      // careful path (the stream's last 64 bits): every zlib outcome checked per step
-      TOK_PC(2);
-      ein_refill(in);
-      uint32_t L, idx, hi = 0;
-      const uint32_t v = ein_rev15(in);
-      const bool ok = huffp_lookup<true>(hl, v, L, idx, hi);
-      if (!ok) {
-        if (ein_avail(in) >= 1u) { rc = INF_DATA; goto done; }
-        goto leave;
-      }
-      if (L > ein_avail(in)) goto leave;
-      const uint32_t sym = (uint32_t)syms_ll[idx] | hi;
-      ein_drop(in, L);
-      if (sym < 256u) {
-        if (op == isize) goto leave;
-        sink.literal(op++, sym);
-        continue;
-      }
-      if (sym == 256u) break;  // end of block
-      if (sym > 285u) { rc = INF_DATA; goto done; }
-      uint32_t lbase, lext;
-      length_base(sym, lbase, lext);
-      if (lext > ein_avail(in)) goto leave;
-      const uint32_t mlen = lbase + ein_peek(in, lext);
-      ein_drop(in, lext);
-      ein_refill(in);
-      const uint32_t vd = ein_rev15(in);
-      uint32_t dh;
-      const bool okd = huffp_lookup<false>(hd, vd, L, idx, dh);
-      if (!okd) {
-        if (ein_avail(in) >= 1u) { rc = INF_DATA; goto done; }
-        goto leave;
-      }
-      if (L > ein_avail(in)) goto leave;
-      const uint32_t dsym = syms_d[idx];
-      ein_drop(in, L);
-      if (dsym > 29u) { rc = INF_DATA; goto done; }
-      uint32_t dbase, dext;
-      dist_base(dsym, dbase, dext);
-      if (dext > ein_avail(in)) goto leave;
-      const uint32_t dist = dbase + ein_peek(in, dext);
-      ein_drop(in, dext);
-      if (op == isize) goto leave;
-      if (dist > op) { rc = INF_DATA; goto done; }
-      uint32_t n = isize - op;
-      n = mlen < n ? mlen : n;
-      sink.match(op, n, dist);
-      op += n;
-      if (n < mlen) goto leave;
-      TOK_PT(7);
     }
   }
 leave:

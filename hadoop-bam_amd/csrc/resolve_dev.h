@@ -36,6 +36,45 @@ constexpr uint32_t RS_BUF = RS_W + 2 * RS_S + 48;     // + pad for 32-byte over-
 static_assert(RS_W >= 16 && RS_W % 16 == 0 && (RS_S == 1024 || RS_S == 2048),
               "window: whole 16-byte columns; stretch: 1 or 2 KiB (one or two columns per lane)");
 constexpr uint32_t RS_MAXM = RS_S / 3 + 2;            // matches starting in one stretch
+constexpr uint32_t RS_PW = (RS_S + 16 + 258 + 31) / 32 + 1;  // pending-byte words of a stretch + spill
+
+constexpr uint32_t RS_SLOTS = (RS_MAXM + 63) / 64;      // ordered matches per lane, at most
+
+// One wave per workgroup: LDS operations of a wave execute in issue order, so ordering the
+// lanes' LDS accesses needs no s_barrier, only that the compiler keep program order across
+// lanes (a workgroup fence + wave barrier).
+__device__ __forceinline__ void rs_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// set / clear bits [x, x + n) of an LDS bitmap (other lanes touch the same words: atomics)
+__device__ __forceinline__ void rs_bits(uint32_t* bm, uint32_t x, uint32_t n, bool set) {
+  uint32_t w = x >> 5, o = x & 31u;
+  while (n) {
+    const uint32_t k = n < 32u - o ? n : 32u - o;
+    const uint32_t m = (k == 32u ? ~0u : ((1u << k) - 1u)) << o;
+    if (set) atomicOr(bm + w, m);
+    else atomicAnd(bm + w, ~m);
+    n -= k;
+    ++w;
+    o = 0;
+  }
+}
+// any bit of [x, y) set
+__device__ __forceinline__ bool rs_any_bit(const uint32_t* bm, uint32_t x, uint32_t y) {
+  uint32_t w = x >> 5, o = x & 31u;
+  uint32_t n = y - x;
+  while (n) {
+    const uint32_t k = n < 32u - o ? n : 32u - o;
+    const uint32_t m = (k == 32u ? ~0u : ((1u << k) - 1u)) << o;
+    if (bm[w] & m) return true;
+    n -= k;
+    ++w;
+    o = 0;
+  }
+  return false;
+}
 
 __device__ __forceinline__ uint64_t lds_rd64(const uint8_t* p) { return *(const uint64_t*)p; }
 

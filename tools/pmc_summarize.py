@@ -26,7 +26,7 @@ def main():
     # the decode of the whole file is the largest dispatch (smaller ones: header probe)
     fetch = 2.0 * 1024.0 * max(f)
     write = 1024.0 * max(w)
-    res = {"kernel": kern, "comp_bytes": int(comp), "dispatches": [len(f), len(w)],
+    res = {"kernel": kern, "tree": "round2", "comp_bytes": int(comp), "dispatches": [len(f), len(w)],
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": fetch + write,
            "note": "FETCH_SIZE x2 (gfx950 16-B/lane read correction), KiB -> B"}

@@ -62,7 +62,8 @@ if a.prof:
         d = (en - st)[ok] / 100.0
         print("  dur_us     mean %10.2f  p50 %10.2f  p99 %10.2f  max %10.2f"
               % (d.mean(), np.percentile(d, 50), np.percentile(d, 99), d.max()))
-    for nm, c in (("stage", 3), ("desc", 4), ("batches", 5), ("n_batch", 6), ("n_match", 7)):
+    for nm, c in (("stage", 3), ("desc", 4), ("batches", 5), ("  of which pre", 12), ("writeback", 13),
+                  ("n_batch", 6), ("n_match", 7)):
         stats(nm, c)
     print("  cycles/batch %.1f, matches/batch %.2f" % (P[:, 5].sum() / max(P[:, 6].sum(), 1),
                                                      P[:, 7].sum() / max(P[:, 6].sum(), 1)))
