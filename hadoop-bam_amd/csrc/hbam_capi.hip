@@ -122,13 +122,21 @@ enum BufId {
 
 }  // namespace
 
+#ifndef HBAM_INFLATE_SLICES
+#define HBAM_INFLATE_SLICES 1  // A/B at 10 GB: 1 -> 163.4 ms, 2 -> 161.5, 4 -> 166.5, 8 -> 164.5 (Huffman + LZ77)
+#endif
+#define HBAM_MAX_SLICES 16
 struct hbam_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hbam_opts opts{};
   std::string err;
   Buf bufs[B_COUNT_ALL];
+  hipStream_t stream2 = nullptr;  // LZ77 pass of slice s beside the Huffman pass of slice s+1
   hipEvent_t ev[16];
+  hipEvent_t slice_ev[HBAM_MAX_SLICES + 1];
+  uint32_t inflate_slices = HBAM_INFLATE_SLICES;  // env HBAM_INFLATE_SLICES overrides (A/B)
+  bool slices_forced = false;                     // ... and then applies to small calls too
   hbam_timing timing{};
   uint64_t* pinned_small = nullptr;  // host pinned scalars
   uint64_t guess_batch = HBAM_GUESS_BATCH;  // env HBAM_GUESS_BATCH overrides (tests: multi-batch)
@@ -397,12 +405,37 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   if ((rc = ensure(c, B_BITMAP, nb * BITMAP_WORDS, &bitmap))) return rc;
   if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
   if ((rc = ensure(c, B_EDGE, 32 * nb + 32, &edges))) return rc;
+  // Both passes are latency-bound at low occupancy (Huffman: 2 waves/SIMD; LZ77: a serial
+  // walk per block), so the blocks are cut into slices and the LZ77 pass of slice s runs on a
+  // second stream beside the Huffman pass of slice s+1: the CUs interleave the two kernels'
+  // waves.  Slices share at most the 16-byte chunk at their boundary, whose bytes each side
+  // writes bytewise (edge merge / LZ77 write-back), never the other side's.
+  uint32_t ns = c->inflate_slices;
+  if (ns < 1) ns = 1;
+  if (ns > HBAM_MAX_SLICES) ns = HBAM_MAX_SLICES;
+  if (!c->slices_forced && nb < (uint64_t)ns * 8192) ns = 1;  // small calls: one slice
+  if (nb < ns) ns = 1;
   if (nb) {
-    k_inflate_tokens<<<grid_for(nb, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
-        dcomp, blk, uoff, (uint32_t)nb, ubuf, lens, bitmap, tails, edges, st);
-    k_edge_merge<<<grid_for(2 * nb, 256), 256, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, edges);
-    HIPCHK(c, hipEventRecord(c->ev[11], c->stream));
-    k_resolve<<<(uint32_t)nb, 64, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, bitmap, tails, st);
+    for (uint32_t si = 0; si < ns; ++si) {
+      const uint64_t lo = nb * si / ns, hi = nb * (si + 1) / ns, n = hi - lo;
+      if (!n) continue;
+      hipStream_t rs = ns > 1 ? c->stream2 : c->stream;
+      k_inflate_tokens<<<grid_for(n, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
+          dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf, lens + lo * LENS_SLOT, bitmap + lo * BITMAP_WORDS,
+          tails + 2 * lo, edges + 32 * lo, st + lo);
+      if (ns > 1) {
+        HIPCHK(c, hipEventRecord(c->slice_ev[si], c->stream));
+        HIPCHK(c, hipStreamWaitEvent(rs, c->slice_ev[si], 0));
+      }
+      if (si + 1 == ns) HIPCHK(c, hipEventRecord(c->ev[11], c->stream));
+      k_edge_merge<<<grid_for(2 * n, 256), 256, 0, rs>>>(blk + lo, uoff + lo, (uint32_t)n, ubuf, edges + 32 * lo);
+      k_resolve<<<(uint32_t)n, 64, 0, rs>>>(blk + lo, uoff + lo, (uint32_t)n, ubuf, bitmap + lo * BITMAP_WORDS,
+                                            tails + 2 * lo, st + lo);
+    }
+    if (ns > 1) {
+      HIPCHK(c, hipEventRecord(c->slice_ev[HBAM_MAX_SLICES], c->stream2));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->slice_ev[HBAM_MAX_SLICES], 0));
+    }
   }
   HIPCHK(c, hipGetLastError());
   if (want_crc && nb) {
@@ -430,7 +463,20 @@ hbam_ctx* hbam_create(int device_ordinal, const hbam_opts* opts) {
     delete c;
     return nullptr;
   }
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return nullptr;
+  }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
+  for (auto& e : c->slice_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  if (const char* sl = getenv("HBAM_INFLATE_SLICES")) {
+    const long v = strtol(sl, nullptr, 10);
+    if (v > 0) {
+      c->inflate_slices = (uint32_t)v;
+      c->slices_forced = true;
+    }
+  }
   if (const char* gb = getenv("HBAM_GUESS_BATCH")) {
     const long v = strtol(gb, nullptr, 10);
     if (v > 0) c->guess_batch = (uint64_t)v;
@@ -448,8 +494,11 @@ void hbam_destroy(hbam_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   for (auto& b : c->bufs)
     if (b.p) (void)hipFree(b.p);
+  (void)hipStreamSynchronize(c->stream2);
   for (auto& e : c->ev) (void)hipEventDestroy(e);
+  for (auto& e : c->slice_ev) (void)hipEventDestroy(e);
   if (c->pinned_small) (void)hipHostFree(c->pinned_small);
+  (void)hipStreamDestroy(c->stream2);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }

@@ -39,6 +39,30 @@ def test_scan_and_inflate_bit_exact(gpu_ctx, oracle_mod, name):
     assert u.tobytes() == want
 
 
+def test_terminator_known_answer_on_device(gpu_ctx, oracle_mod):
+    """The reference's bgzf-terminator.bin through the HIP path: the device block scan finds
+    one 28-byte block of ISIZE 0 and CRC 0, the device inflate yields 0 bytes with status OK,
+    and a BAM whose records are followed by terminators (one mid-file, one at the end) decodes
+    to the same records as the oracle reads (an empty block ends nothing but a read() call)."""
+    t = np.fromfile(os.path.join(GOLDEN, "bgzf-terminator.bin"), np.uint8)
+    rc, b = gpu_ctx.scan_blocks(t)
+    assert rc == 0
+    assert list(b["coff"]) == [0] and list(b["clen"]) == [28] and list(b["isize"]) == [0]
+    assert list(b["crc"]) == [0]
+    rc, u, off, st = gpu_ctx.inflate(t, b, check_crc=True)
+    assert rc == 0 and list(st) == [0] and int(off[-1]) == 0
+    assert gpu_ctx.guess_bgzf_block_start(t, 0, len(t)) == oracle_mod.guess_bgzf_block_start(t, 0, len(t))
+    data = _load("small_pe.bam")
+    blocks = oracle_mod.scan_blocks(data)
+    cut = int(blocks["coff"][len(blocks["coff"]) // 2])
+    twice = np.concatenate([data[:cut], t, data[cut:], t])
+    h = oracle_mod.read_header(twice)
+    ref = oracle_mod.read_split(twice, h["first_voffset"], _whole(twice))
+    got = gpu_ctx.decode_split(twice, h["first_voffset"], _whole(twice), n_ref=-1)
+    assert got["rc"] == 0, got
+    assert_same_split(got, ref)
+
+
 def _bgzf_block(payload, level=6):
     """One BGZF block (BSIZE/CRC/ISIZE as htsjdk writes them) holding `payload`."""
     import struct
@@ -114,6 +138,25 @@ def test_inflate_corrupted_blocks_match_zlib_classes(gpu_ctx, oracle_mod):
         if orc == 0:
             assert u[int(off[i]):int(off[i + 1])].tobytes() == out
     assert len(set(int(x) for x in st)) >= 2  # the corruption exercised error paths
+
+
+@pytest.mark.parametrize("slices", [2, 3, 7])
+def test_sliced_inflate_pipeline(oracle_mod, monkeypatch, slices):
+    """The Huffman / LZ77 passes cut into slices on two streams (HBAM_INFLATE_SLICES forces it
+    on small files): a whole-file decode equals the oracle's."""
+    from hadoop_bam import _lib
+    monkeypatch.setenv("HBAM_INFLATE_SLICES", str(slices))
+    ctx = _lib.Context(0)
+    try:
+        for name in ("small_pe.bam", "edge_uniform_long.bam"):
+            data = _load(name)
+            h = oracle_mod.read_header(data)
+            ref = oracle_mod.read_split(data, h["first_voffset"], _whole(data))
+            got = ctx.decode_split(data, h["first_voffset"], _whole(data), n_ref=-1)
+            assert got["rc"] == 0, got
+            assert_same_split(got, ref)
+    finally:
+        ctx.close()
 
 
 # ---- K5-K8: record reader over splits -------------------------------------------------

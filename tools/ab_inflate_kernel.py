@@ -19,6 +19,7 @@ ap.add_argument("--size", type=float, default=2e9)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--seed", type=int, default=2)
 ap.add_argument("--libs", nargs="+", default=["libhbam.so"])
+ap.add_argument("--slices", nargs="+", type=int, default=[0], help="HBAM_INFLATE_SLICES values (0: library default)")
 a = ap.parse_args()
 g = genbam.generate(target_bytes=int(a.size), seed=a.seed, threads=16)
 data = np.asarray(g)
@@ -26,7 +27,11 @@ d = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
 d[:len(data)].copy_(torch.from_numpy(data))
 d[len(data):].zero_()
 torch.cuda.synchronize()
-for lib in a.libs:
+for lib, sl in [(x, y) for x in a.libs for y in a.slices]:
+    if sl:
+        os.environ["HBAM_INFLATE_SLICES"] = str(sl)
+    else:
+        os.environ.pop("HBAM_INFLATE_SLICES", None)
     _lib._LIB = None
     L = _lib.load(os.path.join(ROOT, "hadoop-bam_amd", lib))
     ctx = _lib.Context(0)
@@ -43,7 +48,7 @@ for lib in a.libs:
         rc = L.hbam_inflate(ctx.h, C.c_void_p(d.data_ptr()), 1, len(data), arr, n, 0, None, 0,
                             off.ctypes.data, st.ctypes.data)
         t = ctx.timing()
-        print("%-28s rep %d rc %d blocks %d U %.3f GB huffman %.3f ms resolve %.3f ms bad %d"
-              % (lib, r, rc, n, off[-1] / 1e9, t["huffman_ms"], t["resolve_ms"], int(np.sum(st != 0))),
+        print("%-18s slices %d rep %d rc %d blocks %d U %.3f GB huffman %.3f ms resolve %.3f ms bad %d"
+              % (lib, sl, r, rc, n, off[-1] / 1e9, t["huffman_ms"], t["resolve_ms"], int(np.sum(st != 0))),
               flush=True)
     ctx.close()

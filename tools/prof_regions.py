@@ -16,6 +16,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "hadoop-bam_amd"), os.path.join(ROOT, "tools")]
 os.environ["HBAM_LIB"] = os.path.join(ROOT, "hadoop-bam_amd", "libhbam_prof.so")
+os.environ["HBAM_INFLATE_SLICES"] = "1"  # per-block prof slots are indexed per launch
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

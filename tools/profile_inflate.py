@@ -21,6 +21,7 @@ ap.add_argument("--prof", action="store_true",
 a = ap.parse_args()
 if a.prof:
     os.environ["HBAM_LIB"] = os.path.join(ROOT, "hadoop-bam_amd", "libhbam_prof.so")
+    os.environ["HBAM_INFLATE_SLICES"] = "1"  # per-block prof slots are indexed per launch
 g = genbam.generate(target_bytes=int(a.size), seed=a.seed, threads=16)
 data = np.asarray(g)
 d = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
