@@ -313,9 +313,11 @@ class Context:
         out["timing"] = self.timing()
         return out
 
-    def split_stream(self, data, v_start, v_end, n_ref, window_bytes=1 << 30):
+    def split_stream(self, data, v_start, v_end, n_ref, window_bytes=1 << 30, host=True):
         """Streamed BAMRecordReader over a host-resident file (hbam_split_open/next): yields
-        the host columns of each window in order; the last one carries the split's status."""
+        the host columns of each window in order; the last one carries the split's status.
+        host=False yields each window's device Columns struct instead (valid until the next
+        window is requested)."""
         a = np.ascontiguousarray(np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray)
                                  else data, dtype=np.uint8)
         keep = a if a.size else np.zeros(1, np.uint8)
@@ -331,6 +333,9 @@ class Context:
                     raise RuntimeError("hbam_split_next failed (%d): %s" % (rc, self.last_error()))
                 if rc == 0:
                     return
+                if not host:
+                    yield d
+                    continue
                 h = Columns()
                 rc = self.L.hbam_columns_to_host(self.h, C.byref(d), C.byref(h))
                 if rc:
