@@ -23,6 +23,7 @@
 #include "hbam_kernels.hip"
 #include "hbam_guess.hip"
 #include "hbam_sort.hip"
+#include "hbam_deflate.hip"
 
 using namespace hbam;
 
@@ -117,6 +118,15 @@ enum BufId {
   B_S_PERM,
   B_S_RECOFF,
   B_S_BOUNDS,
+  B_DF_SRC,
+  B_DF_TOK,
+  B_DF_NTOK,
+  B_DF_FREQ,
+  B_DF_CRC,
+  B_DF_SLOTS,
+  B_DF_CSIZE,
+  B_DF_OFF,
+  B_DF_DST,
   B_COUNT_ALL
 };
 
@@ -1844,3 +1854,76 @@ extern "C" int hbam_prof_attach_guess(void* dev) {
   return hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_gprof), &p, sizeof p) == hipSuccess ? 0 : -1;
 }
 #endif
+
+// =====================================================================================
+// BGZF compression (hbam_deflate.hip): BlockCompressedOutputStream for the BAM writer.
+namespace {
+constexpr uint32_t DF_BATCH = 4096;  // blocks per launch: ~1 GiB of token scratch
+}
+
+extern "C" uint64_t hbam_bgzf_bound(uint64_t n, uint32_t block_size) {
+  const uint32_t bs = block_size ? block_size : hbam::DF_MAXB;
+  return ((n + bs - 1) / bs) * (uint64_t)hbam::DF_SLOT;
+}
+
+extern "C" int64_t hbam_bgzf_compress(hbam_ctx* c, const uint8_t* src, int src_on_device, uint64_t n,
+                                      uint32_t block_size, uint8_t* dst, int dst_on_device, uint64_t dst_cap) {
+  if (!c || (n && (!src || !dst))) return HBAM_EINVAL;
+  const uint32_t bs = block_size ? block_size : DF_MAXB;
+  if (bs > DF_MAXB || bs < 1024) return set_err(c, HBAM_EINVAL, "block_size %u not in [1024, %u]", bs, DF_MAXB);
+  HIPCHK(c, hipSetDevice(c->device));
+  if (n == 0) return 0;
+  const uint8_t* d;
+  int rc;
+  if (src_on_device) {
+    d = src;
+  } else {
+    uint8_t* ds;
+    if ((rc = ensure(c, B_DF_SRC, n + 64, &ds))) return rc;
+    HIPCHK(c, hipMemcpyAsync(ds, src, n, hipMemcpyHostToDevice, c->stream));
+    d = ds;
+  }
+  const uint64_t nb = (n + bs - 1) / bs;
+  uint64_t out_total = 0;
+  HIPCHK(c, hipEventRecord(c->ev[9], c->stream));
+  for (uint64_t b0 = 0; b0 < nb; b0 += DF_BATCH) {
+    const uint32_t k = (uint32_t)std::min<uint64_t>(DF_BATCH, nb - b0);
+    const uint64_t off0 = b0 * bs;
+    const uint64_t nn = std::min<uint64_t>(n - off0, (uint64_t)k * bs);
+    uint32_t *tok, *ntok, *freq, *crc, *csize;
+    uint8_t* slots;
+    uint64_t* off;
+    if ((rc = ensure(c, B_DF_TOK, (uint64_t)k * bs, &tok)) || (rc = ensure(c, B_DF_NTOK, k, &ntok)) ||
+        (rc = ensure(c, B_DF_FREQ, (uint64_t)k * DF_NSYM, &freq)) || (rc = ensure(c, B_DF_CRC, k, &crc)) ||
+        (rc = ensure(c, B_DF_SLOTS, (uint64_t)k * DF_SLOT, &slots)) || (rc = ensure(c, B_DF_CSIZE, k + 1, &csize)) ||
+        (rc = ensure(c, B_DF_OFF, k + 1, &off)))
+      return rc;
+    k_crc_blocks<<<grid_for(k, 256), 256, 0, c->stream>>>(d + off0, nn, bs, k, crc);
+    k_lz77_tokens<<<k, DF_WG, 0, c->stream>>>(d + off0, nn, bs, k, tok, ntok, freq);
+    k_deflate_encode<<<k, DF_WG, 0, c->stream>>>(d + off0, nn, bs, k, tok, ntok, freq, crc, slots, csize);
+    HIPCHK(c, hipGetLastError());
+    uint64_t bytes = 0;
+    if ((rc = scan_exclusive<uint32_t>(c, csize, k, off, &bytes))) return rc;
+    if (out_total + bytes > dst_cap)
+      return set_err(c, HBAM_EINVAL, "dst_cap %llu < %llu compressed bytes", (unsigned long long)dst_cap,
+                     (unsigned long long)(out_total + bytes));
+    uint8_t* pd;
+    if (dst_on_device) {
+      pd = dst + out_total;
+    } else {
+      if ((rc = ensure(c, B_DF_DST, bytes + 64, &pd))) return rc;
+    }
+    k_pack_members<<<k, 256, 0, c->stream>>>(slots, csize, off, k, pd);
+    HIPCHK(c, hipGetLastError());
+    if (!dst_on_device) HIPCHK(c, hipMemcpyAsync(dst + out_total, pd, bytes, hipMemcpyDeviceToHost, c->stream));
+    out_total += bytes;
+  }
+  HIPCHK(c, hipEventRecord(c->ev[10], c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->timing = hbam_timing{};
+  c->timing.total_ms = ev_ms(c, 9, 10);
+  c->timing.ubuf_bytes = n;
+  c->timing.comp_bytes = out_total;
+  c->timing.n_blocks = nb;
+  return (int64_t)out_total;
+}

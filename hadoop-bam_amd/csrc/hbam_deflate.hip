@@ -1,0 +1,563 @@
+// hbam_deflate.hip — BGZF block compression on the device: the
+// BlockCompressedOutputStream under BAMRecordWriter (BAMRecordWriter.java:96-111) and
+// SAMOutputPreparer (util/SAMOutputPreparer.java:58-95), for the Sort plugin's output.
+//
+// The uncompressed stream is cut into blocks of `bsize` bytes; every block becomes one
+// independent BGZF member (RFC 1952 header with the BC extra field, one raw DEFLATE stream,
+// CRC32, ISIZE).  Parity is defined on the inflated bytes: any valid
+// DEFLATE stream is accepted by htsjdk's reader, so the compressor is free to be GPU-shaped.
+//
+//   k_lz77_tokens (one 256-thread workgroup per block): the block is staged in LDS; for every
+//     256-position chunk each thread finds the longest match at its position among the most
+//     recent earlier position with the same 4-byte hash (from earlier chunks) and the four
+//     previous positions (byte / short-period runs); wave 0 then walks the chunk greedily
+//     with readlane (the parse is serial, the data already in registers), emitting tokens
+//     to a per-block global buffer and symbol frequencies to LDS.
+//   k_deflate_encode (one 256-thread workgroup per block): length-limited Huffman codes from
+//     the frequencies (lit/len ≤ 15, distance ≤ 15, code-length code ≤ 7), the dynamic-block
+//     header, then every token's bit offset by a block-wide scan and its bits OR-ed into an
+//     LDS output image; a block that does not shrink is written as a stored block.  The
+//     BGZF member goes to a 64 KiB slot; a scan + copy packs the slots.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hbam_internal.h"
+
+namespace hbam {
+
+constexpr uint32_t DF_WG = 256;
+constexpr uint32_t DF_MAXB = 65280;           // largest block accepted (bgzip's 0xff00)
+constexpr uint32_t DF_HBITS = 11;             // 2048-entry hash heads
+constexpr uint32_t DF_SLOT = 65536;           // BGZF member slot (BSIZE <= 65536)
+constexpr uint32_t DF_NSYM = 286 + 30;        // lit/len + distance frequencies per block
+constexpr uint32_t DF_WINDOW = 32768;
+
+__device__ __forceinline__ uint32_t df_hash(uint32_t w) { return (w * 2654435761u) >> (32 - DF_HBITS); }
+
+__device__ __forceinline__ uint32_t df_rd32(const uint8_t* s, uint32_t p) {
+  return (uint32_t)s[p] | (uint32_t)s[p + 1] << 8 | (uint32_t)s[p + 2] << 16 | (uint32_t)s[p + 3] << 24;
+}
+
+// length of the common prefix of s[a..] and s[p..], at most lim
+__device__ __forceinline__ uint32_t df_match(const uint8_t* s, uint32_t a, uint32_t p, uint32_t lim) {
+  uint32_t l = 0;
+  while (l + 4 <= lim) {
+    const uint32_t x = df_rd32(s, a + l) ^ df_rd32(s, p + l);
+    if (x) return l + (__builtin_ctz(x) >> 3);
+    l += 4;
+  }
+  while (l < lim && s[a + l] == s[p + l]) ++l;
+  return l;
+}
+
+// RFC 1951 length code of a match length 3..258: symbol, extra bits, extra value
+__device__ __forceinline__ void df_len_code(uint32_t len, uint32_t& sym, uint32_t& eb, uint32_t& ev) {
+  if (len == 258) {
+    sym = 285; eb = 0; ev = 0;
+    return;
+  }
+  const uint32_t x = len - 3;
+  if (x < 8) {
+    sym = 257 + x; eb = 0; ev = 0;
+    return;
+  }
+  eb = 31 - __builtin_clz(x) - 2;  // x in [8, 255]: 1..5 extra bits
+  const uint32_t base = (4u + ((x >> eb) & 3u)) << eb;
+  sym = 257 + 4 * eb + 4 + ((x >> eb) & 3u);
+  ev = x - base;
+}
+// distance code of 1..32768
+__device__ __forceinline__ void df_dist_code(uint32_t d, uint32_t& sym, uint32_t& eb, uint32_t& ev) {
+  const uint32_t x = d - 1;
+  if (x < 4) {
+    sym = x; eb = 0; ev = 0;
+    return;
+  }
+  eb = 31 - __builtin_clz(x) - 1;  // x in [4, 32767]: 1..13 extra bits
+  const uint32_t hb = (x >> eb) & 1u;
+  sym = 2 * eb + 2 + hb;
+  ev = x - ((2u + hb) << eb);
+}
+
+// token: literal = byte; match = 1<<31 | len<<16 | dist (dist <= 32768, len <= 258)
+__global__ __launch_bounds__(DF_WG) void k_lz77_tokens(const uint8_t* __restrict__ src, uint64_t n,
+                                                       uint32_t bsize, uint32_t nblk,
+                                                       uint32_t* __restrict__ tok,
+                                                       uint32_t* __restrict__ ntok,
+                                                       uint32_t* __restrict__ freq) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[DF_MAXB + 288];
+  __shared__ uint32_t s_head[1u << DF_HBITS];
+  __shared__ uint32_t s_ml[DF_WG];
+  __shared__ uint32_t s_freq[DF_NSYM];
+  const uint32_t b = blockIdx.x, t = threadIdx.x, lane = t & 63u;
+  if (b >= nblk) return;
+  const uint64_t start = (uint64_t)b * bsize;
+  const uint32_t len = (uint32_t)((n - start) < bsize ? (n - start) : bsize);
+  for (uint32_t i = t; i < (DF_MAXB + 288) / 4; i += DF_WG) {
+    const uint32_t p = 4 * i;
+    uint32_t w = 0;
+    if (p + 4 <= len) {
+      w = df_rd32(src + start, p);  // byte loads: src has no alignment guarantee
+    } else {
+      for (uint32_t k = 0; k < 4; ++k)
+        if (p + k < len) w |= (uint32_t)src[start + p + k] << (8 * k);
+    }
+    ((uint32_t*)s_in)[i] = w;
+  }
+  for (uint32_t i = t; i < (1u << DF_HBITS); i += DF_WG) s_head[i] = 0;
+  for (uint32_t i = t; i < DF_NSYM; i += DF_WG) s_freq[i] = 0;
+  __syncthreads();
+  uint32_t* out = tok + (uint64_t)b * bsize;
+  uint32_t nxt = 0, nt = 0;  // parse position / tokens emitted (wave 0, uniform)
+  uint32_t tbuf = 0;         // wave 0: the next 64 tokens, one per lane
+  for (uint32_t c0 = 0; c0 < len; c0 += DF_WG) {
+    const uint32_t p = c0 + t;
+    uint32_t best = 0;
+    uint32_t h = 0;
+    const bool has4 = p + 4 <= len;
+    if (has4) {
+      const uint32_t lim = (len - p) < 258u ? (len - p) : 258u;
+      h = df_hash(df_rd32(s_in, p));
+      uint32_t bl = 0, bd = 0;
+      // short periods first: runs of one byte and of short repeats are the commonest match
+#pragma unroll
+      for (uint32_t d = 1; d <= 4; ++d) {
+        if (p >= d) {
+          const uint32_t m = df_match(s_in, p - d, p, lim);
+          if (m > bl) {
+            bl = m;
+            bd = d;
+          }
+        }
+      }
+      const uint32_t hc = s_head[h];
+      if (hc) {
+        const uint32_t a = hc - 1;
+        if (p - a <= DF_WINDOW && p - a > 4) {
+          const uint32_t m = df_match(s_in, a, p, lim);
+          if (m > bl) {
+            bl = m;
+            bd = p - a;
+          }
+        }
+      }
+      if (bl >= 4 || (bl == 3 && bd <= 64)) best = 0x80000000u | bl << 16 | bd;
+    }
+    s_ml[t] = best;
+    __syncthreads();
+    if (has4) atomicMax(&s_head[h], p + 1);  // most recent position of the hash, for later chunks
+    if (t < 64) {
+      // greedy parse of this chunk from nxt (uniform across wave 0; the chunk's match info is
+      // read into registers once and walked with readlane)
+      const uint32_t m0 = s_ml[lane], m1 = s_ml[64 + lane], m2 = s_ml[128 + lane], m3 = s_ml[192 + lane];
+      const uint32_t cend = (c0 + DF_WG < len) ? c0 + DF_WG : len;
+      while (nxt < cend) {
+        const uint32_t r = nxt - c0;
+        const uint32_t q = r & 63u;
+        uint32_t m;
+        if (r < 64) m = __builtin_amdgcn_readlane(m0, q);
+        else if (r < 128) m = __builtin_amdgcn_readlane(m1, q);
+        else if (r < 192) m = __builtin_amdgcn_readlane(m2, q);
+        else m = __builtin_amdgcn_readlane(m3, q);
+        uint32_t tk, step;
+        if (m) {
+          tk = m;
+          step = (m >> 16) & 0x1ffu;
+        } else {
+          tk = s_in[nxt];
+          step = 1;
+        }
+        if (lane == (nt & 63u)) tbuf = tk;
+        if (lane == 0) {
+          if (m) {
+            uint32_t sy, eb, ev;
+            df_len_code(step, sy, eb, ev);
+            atomicAdd(&s_freq[sy], 1u);
+            df_dist_code(m & 0xffffu, sy, eb, ev);
+            atomicAdd(&s_freq[286 + sy], 1u);
+          } else {
+            atomicAdd(&s_freq[tk], 1u);
+          }
+        }
+        ++nt;
+        if ((nt & 63u) == 0) out[nt - 64 + lane] = tbuf;
+        nxt += step;
+      }
+    }
+    __syncthreads();
+  }
+  if (t < 64) {
+    if (lane < (nt & 63u)) out[(nt & ~63u) + lane] = tbuf;
+    if (t == 0) {
+      ntok[b] = nt;
+      atomicAdd(&s_freq[256], 1u);  // end of block
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < DF_NSYM; i += DF_WG) freq[(uint64_t)b * DF_NSYM + i] = s_freq[i];
+}
+
+// ---- Huffman code lengths (one thread): Huffman tree by two queues over the symbols sorted
+// by frequency, then lengths limited to maxl.  sorted[] / wt[] / par[] are LDS scratch.
+__device__ void df_lengths(const uint32_t* f, uint32_t n, uint32_t maxl, uint8_t* len,
+                           uint16_t* sorted, uint32_t* wt, uint16_t* par, uint32_t m) {
+  // m = number of used symbols (listed in sorted[0..m) by ascending frequency)
+  for (uint32_t i = 0; i < n; ++i) len[i] = 0;
+  if (m == 0) return;
+  if (m == 1) {
+    len[sorted[0]] = 1;
+    return;
+  }
+  // nodes: 0..m-1 leaves (in sorted order), m..2m-2 internal; two-queue merge
+  for (uint32_t i = 0; i < m; ++i) wt[i] = f[sorted[i]];
+  uint32_t ql = 0, qi = m, ni = m;
+  for (uint32_t k = 0; k < m - 1; ++k) {
+    uint32_t pick[2];
+    for (int j = 0; j < 2; ++j) {
+      if (ql < m && (qi >= ni || wt[ql] <= wt[qi])) pick[j] = ql++;
+      else pick[j] = qi++;
+    }
+    wt[ni] = wt[pick[0]] + wt[pick[1]];
+    par[pick[0]] = (uint16_t)ni;
+    par[pick[1]] = (uint16_t)ni;
+    ++ni;
+  }
+  // depths: root = ni - 1
+  uint32_t* dep = wt;  // reuse: depth of node i (computed top-down: parents have larger ids)
+  dep[ni - 1] = 0;
+  for (int i = (int)ni - 2; i >= 0; --i) dep[i] = dep[par[i]] + 1;
+  // bit-length counts with zlib's overflow repair (trees.c gen_bitlen): a leaf deeper than
+  // maxl is moved up beside a shallower leaf, which keeps the Kraft sum exactly 1 (a complete
+  // code: inflate rejects incomplete lit/len and code-length sets)
+  uint32_t cnt[16];
+  for (int L = 0; L < 16; ++L) cnt[L] = 0;
+  int overflow = 0;
+  for (uint32_t i = 0; i < m; ++i) {
+    uint32_t d = dep[i];
+    if (d > maxl) {
+      d = maxl;
+      ++overflow;
+    }
+    ++cnt[d];
+  }
+  while (overflow > 0) {
+    uint32_t L = maxl - 1;
+    while (cnt[L] == 0) --L;
+    --cnt[L];
+    cnt[L + 1] += 2;
+    --cnt[maxl];
+    overflow -= 2;
+  }
+  // lengths by frequency: the least frequent symbols (front of sorted[]) get the longest codes
+  uint32_t k = 0;
+  for (uint32_t L = maxl; L >= 1; --L)
+    for (uint32_t c = 0; c < cnt[L]; ++c) len[sorted[k++]] = (uint8_t)L;
+}
+
+// canonical codes, bit-reversed for the LSB-first bit stream
+__device__ void df_codes(const uint8_t* len, uint32_t n, uint16_t* code) {
+  uint32_t cnt[16], next[16];
+  for (int L = 0; L < 16; ++L) cnt[L] = 0;
+  for (uint32_t i = 0; i < n; ++i) ++cnt[len[i]];
+  cnt[0] = 0;
+  uint32_t c = 0;
+  for (int L = 1; L < 16; ++L) {
+    c = (c + cnt[L - 1]) << 1;
+    next[L] = c;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t L = len[i];
+    if (!L) {
+      code[i] = 0;
+      continue;
+    }
+    const uint32_t v = next[L]++;
+    code[i] = (uint16_t)(__builtin_bitreverse32(v) >> (32 - L));
+  }
+}
+
+// sort used symbols by (frequency, symbol) ascending into sorted[], parallel ranks
+__device__ uint32_t df_sort_used(const uint32_t* f, uint32_t n, uint16_t* sorted, uint32_t t) {
+  __shared__ uint32_t s_m;
+  if (t == 0) s_m = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < n; i += DF_WG) {
+    if (!f[i]) continue;
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j)
+      r += (f[j] && (f[j] < f[i] || (f[j] == f[i] && j < i))) ? 1u : 0u;
+    sorted[r] = (uint16_t)i;
+    atomicAdd(&s_m, 1u);
+  }
+  __syncthreads();
+  return s_m;
+}
+
+struct DfBits {  // serial bit writer into the LDS image (one thread)
+  uint32_t* w;
+  uint32_t pos;
+  __device__ void put(uint32_t v, uint32_t nb) {
+    if (!nb) return;
+    const uint64_t x = (uint64_t)v << (pos & 31u);
+    w[pos >> 5] |= (uint32_t)x;
+    if ((pos & 31u) + nb > 32u) w[(pos >> 5) + 1] |= (uint32_t)(x >> 32);
+    pos += nb;
+  }
+};
+
+constexpr uint32_t DF_OUTW = (DF_SLOT + 64) / 4;  // LDS image words
+
+__global__ __launch_bounds__(DF_WG) void k_deflate_encode(const uint8_t* __restrict__ src, uint64_t n,
+                                                          uint32_t bsize, uint32_t nblk,
+                                                          const uint32_t* __restrict__ tok,
+                                                          const uint32_t* __restrict__ ntok,
+                                                          const uint32_t* __restrict__ freq,
+                                                          const uint32_t* __restrict__ crc,
+                                                          uint8_t* __restrict__ slots,
+                                                          uint32_t* __restrict__ csize) {
+  __shared__ uint32_t s_out[DF_OUTW];
+  __shared__ uint32_t s_f[DF_NSYM];
+  __shared__ uint8_t s_len[DF_NSYM];
+  __shared__ uint16_t s_code[DF_NSYM];
+  __shared__ uint16_t s_sorted[320];
+  __shared__ uint32_t s_wt[640];
+  __shared__ uint16_t s_par[640];
+  __shared__ uint32_t s_clf[19];
+  __shared__ uint8_t s_cll[19];
+  __shared__ uint16_t s_clc[19];
+  __shared__ uint16_t s_rle[320];   // RLE'd code lengths: sym | extra << 5
+  __shared__ uint32_t s_nrle, s_hlit, s_hdist, s_bits, s_wsum[DF_WG / 64];
+  const uint32_t b = blockIdx.x, t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  if (b >= nblk) return;
+  const uint64_t start = (uint64_t)b * bsize;
+  const uint32_t len = (uint32_t)((n - start) < bsize ? (n - start) : bsize);
+  const uint32_t nt = ntok[b];
+  for (uint32_t i = t; i < DF_NSYM; i += DF_WG) s_f[i] = freq[(uint64_t)b * DF_NSYM + i];
+  for (uint32_t i = t; i < DF_OUTW; i += DF_WG) s_out[i] = 0;
+  __syncthreads();
+  if (t == 0) {
+    // a complete lit/len code needs two symbols; the end-of-block symbol is always used
+    uint32_t used = 0;
+    for (uint32_t i = 0; i < 286; ++i) used += s_f[i] ? 1u : 0u;
+    if (used < 2) s_f[s_f[0] ? 1 : 0] += 1;
+  }
+  __syncthreads();
+  // lit/len lengths
+  uint32_t m = df_sort_used(s_f, 286, s_sorted, t);
+  if (t == 0) df_lengths(s_f, 286, 15, s_len, s_sorted, s_wt, s_par, m);
+  __syncthreads();
+  // distance lengths (an empty set is sent as one unused code of length 1)
+  m = df_sort_used(s_f + 286, 30, s_sorted, t);
+  if (t == 0) {
+    df_lengths(s_f + 286, 30, 15, s_len + 286, s_sorted, s_wt, s_par, m);
+    if (m == 0) s_len[286] = 1;
+    df_codes(s_len, 286, s_code);
+    df_codes(s_len + 286, 30, s_code + 286);
+    // HLIT / HDIST and the run-length coded length sequence (RFC 1951 3.2.7)
+    uint32_t hlit = 286;
+    while (hlit > 257 && !s_len[hlit - 1]) --hlit;
+    uint32_t hdist = 30;
+    while (hdist > 1 && !s_len[286 + hdist - 1]) --hdist;
+    s_hlit = hlit;
+    s_hdist = hdist;
+    for (int i = 0; i < 19; ++i) s_clf[i] = 0;
+    uint32_t nr = 0;
+    const uint32_t tot = hlit + hdist;
+    uint32_t i = 0;
+    while (i < tot) {
+      const uint32_t v = i < hlit ? s_len[i] : s_len[286 + i - hlit];
+      uint32_t r = 1;
+      while (i + r < tot && (i + r < hlit ? s_len[i + r] : s_len[286 + i + r - hlit]) == v) ++r;
+      uint32_t left = r;
+      if (v == 0) {
+        while (left >= 11) {
+          const uint32_t k = left < 138 ? left : 138;
+          s_rle[nr++] = (uint16_t)(18 | (k - 11) << 5);
+          ++s_clf[18];
+          left -= k;
+        }
+        if (left >= 3) {
+          s_rle[nr++] = (uint16_t)(17 | (left - 3) << 5);
+          ++s_clf[17];
+          left = 0;
+        }
+      } else {
+        s_rle[nr++] = (uint16_t)v;
+        ++s_clf[v];
+        --left;
+        while (left >= 3) {
+          const uint32_t k = left < 6 ? left : 6;
+          s_rle[nr++] = (uint16_t)(16 | (k - 3) << 5);
+          ++s_clf[16];
+          left -= k;
+        }
+      }
+      while (left) {
+        s_rle[nr++] = (uint16_t)v;
+        ++s_clf[v];
+        --left;
+      }
+      i += r;
+    }
+    s_nrle = nr;
+    // the code-length code must be complete: at least two symbols
+    uint32_t used = 0;
+    for (int k = 0; k < 19; ++k) used += s_clf[k] ? 1u : 0u;
+    if (used < 2) s_clf[s_clf[0] ? 1 : 0] += 1;
+  }
+  __syncthreads();
+  m = df_sort_used(s_clf, 19, s_sorted, t);
+  if (t == 0) {
+    df_lengths(s_clf, 19, 7, s_cll, s_sorted, s_wt, s_par, m);
+    df_codes(s_cll, 19, s_clc);
+    // header
+    DfBits bw{s_out, 0};
+    bw.put(1, 1);  // BFINAL
+    bw.put(2, 2);  // dynamic
+    bw.put(s_hlit - 257, 5);
+    bw.put(s_hdist - 1, 5);
+    const uint8_t ord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    uint32_t hclen = 19;
+    while (hclen > 4 && !s_cll[ord[hclen - 1]]) --hclen;
+    bw.put(hclen - 4, 4);
+    for (uint32_t k = 0; k < hclen; ++k) bw.put(s_cll[ord[k]], 3);
+    for (uint32_t k = 0; k < s_nrle; ++k) {
+      const uint32_t sy = s_rle[k] & 31u, ex = s_rle[k] >> 5;
+      bw.put(s_clc[sy], s_cll[sy]);
+      if (sy == 16) bw.put(ex, 2);
+      else if (sy == 17) bw.put(ex, 3);
+      else if (sy == 18) bw.put(ex, 7);
+    }
+    s_bits = bw.pos;
+  }
+  __syncthreads();
+  // tokens: each round 256 tokens, bit offsets by a block-wide exclusive scan
+  const uint32_t* tk = tok + (uint64_t)b * bsize;
+  uint32_t base = s_bits;
+  bool overflow = false;
+  for (uint32_t r0 = 0; r0 < nt; r0 += DF_WG) {
+    const uint32_t i = r0 + t;
+    uint64_t v = 0;
+    uint32_t nb = 0;
+    if (i < nt) {
+      const uint32_t x = tk[i];
+      if (x & 0x80000000u) {
+        const uint32_t ml = (x >> 16) & 0x1ffu, d = x & 0xffffu;
+        uint32_t sy, eb, ev;
+        df_len_code(ml, sy, eb, ev);
+        v = s_code[sy];
+        nb = s_len[sy];
+        v |= (uint64_t)ev << nb;
+        nb += eb;
+        df_dist_code(d, sy, eb, ev);
+        v |= (uint64_t)s_code[286 + sy] << nb;
+        nb += s_len[286 + sy];
+        v |= (uint64_t)ev << nb;
+        nb += eb;
+      } else {
+        v = s_code[x];
+        nb = s_len[x];
+      }
+    }
+    // exclusive scan of nb over the 256 threads
+    uint32_t inc = nb;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(inc, off);
+      if ((int)lane >= off) inc += y;
+    }
+    if (lane == 63) s_wsum[wv] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+    for (uint32_t k = 0; k < DF_WG / 64; ++k) {
+      if (k < wv) wbase += s_wsum[k];
+      total += s_wsum[k];
+    }
+    const uint32_t pos = base + wbase + inc - nb;
+    if (nb && pos + nb + 16 < 8u * (DF_SLOT - 64)) {
+      const uint32_t w = pos >> 5, sh = pos & 31u;
+      const uint64_t lo = v << sh;
+      const uint32_t hi = sh ? (uint32_t)(v >> (64 - sh)) : 0u;
+      atomicOr(&s_out[w], (uint32_t)lo);
+      if ((uint32_t)(lo >> 32)) atomicOr(&s_out[w + 1], (uint32_t)(lo >> 32));
+      if (hi) atomicOr(&s_out[w + 2], hi);
+    }
+    base += total;
+    if (base + 64 >= 8u * (DF_SLOT - 64)) overflow = true;
+    __syncthreads();
+  }
+  // end of block, then the member
+  uint32_t dbytes = 0;
+  bool stored = overflow;
+  if (!stored) {
+    const uint32_t pos = base;
+    if (t == 0) {
+      DfBits bw{s_out, pos};
+      bw.put(s_code[256], s_len[256]);
+      s_bits = bw.pos;
+    }
+    __syncthreads();
+    dbytes = (s_bits + 7) >> 3;
+    stored = dbytes + 26 > DF_SLOT || dbytes >= len + 5;
+  }
+  uint8_t* slot = slots + (uint64_t)b * DF_SLOT;
+  const uint32_t body = stored ? len + 5 : dbytes;
+  const uint32_t total_sz = body + 26;
+  if (t == 0) {
+    const uint32_t bs1 = total_sz - 1;
+    const uint8_t hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0,
+                             (uint8_t)(bs1 & 0xff), (uint8_t)(bs1 >> 8)};
+    for (int k = 0; k < 18; ++k) slot[k] = hdr[k];
+    const uint32_t c = crc[b];
+    uint8_t* tail = slot + 18 + body;
+    for (int k = 0; k < 4; ++k) tail[k] = (uint8_t)(c >> (8 * k));
+    for (int k = 0; k < 4; ++k) tail[4 + k] = (uint8_t)(len >> (8 * k));
+    if (stored) {  // BFINAL=1 BTYPE=00, byte aligned: LEN, NLEN, the bytes
+      slot[18] = 1;
+      slot[19] = (uint8_t)(len & 0xff);
+      slot[20] = (uint8_t)(len >> 8);
+      slot[21] = (uint8_t)(~len & 0xff);
+      slot[22] = (uint8_t)((~len >> 8) & 0xff);
+    }
+    csize[b] = total_sz;
+  }
+  if (stored) {
+    for (uint32_t i = t; i < len; i += DF_WG) slot[23 + i] = src[start + i];
+  } else {
+    const uint8_t* img = (const uint8_t*)s_out;
+    for (uint32_t i = t; i < dbytes; i += DF_WG) slot[18 + i] = img[i];
+  }
+}
+
+// BGZF members of the blocks -> packed at off[b]
+__global__ void k_pack_members(const uint8_t* __restrict__ slots, const uint32_t* __restrict__ csize,
+                               const uint64_t* __restrict__ off, uint32_t nblk, uint8_t* __restrict__ dst) {
+  const uint32_t b = blockIdx.x;
+  if (b >= nblk) return;
+  const uint32_t sz = csize[b];
+  const uint8_t* s = slots + (uint64_t)b * DF_SLOT;
+  uint8_t* d = dst + off[b];
+  for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) d[i] = s[i];
+}
+
+// CRC-32 of each uncompressed block (blocks of bsize over src), one thread per block
+__global__ __launch_bounds__(256) void k_crc_blocks(const uint8_t* __restrict__ src, uint64_t n, uint32_t bsize,
+                                                    uint32_t nblk, uint32_t* __restrict__ crc_out) {
+  __shared__ uint32_t T[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1u) ? 0xedb88320u ^ (c >> 1) : c >> 1;
+    T[i] = c;
+  }
+  __syncthreads();
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  const uint64_t start = (uint64_t)b * bsize;
+  const uint32_t len = (uint32_t)((n - start) < bsize ? (n - start) : bsize);
+  const uint8_t* p = src + start;
+  uint32_t c = 0xffffffffu;
+  for (uint32_t i = 0; i < len; ++i) c = T[(c ^ p[i]) & 0xffu] ^ (c >> 8);
+  crc_out[b] = ~c;
+}
+
+}  // namespace hbam

@@ -46,7 +46,7 @@ EXPORTS = [
     "hbam_sort_keys", "hbam_gather_records", "hbam_permute", "hbam_splitting_index",
     "hbam_bgzf_block_index", "hbam_resolve_tokens", "hbam_split_open", "hbam_split_next",
     "hbam_split_stats", "hbam_split_close", "hbam_device_alloc", "hbam_sort_split",
-    "hbam_sort_partition", "hbam_sort_received",
+    "hbam_sort_partition", "hbam_sort_received", "hbam_bgzf_bound", "hbam_bgzf_compress",
 ]
 
 
@@ -168,6 +168,9 @@ def load(path=None):
         "hbam_sort_split": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(SortedRunC)]),
         "hbam_sort_partition": (C.c_int, [vp, C.POINTER(SortedRunC), vp, C.c_uint32, vp, vp]),
         "hbam_sort_received": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, C.POINTER(SortedRunC)]),
+        "hbam_bgzf_bound": (C.c_uint64, [C.c_uint64, C.c_uint32]),
+        "hbam_bgzf_compress": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int,
+                                           C.c_uint64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)
@@ -253,6 +256,24 @@ class Context:
             a = np.zeros(1, np.uint8)
             return C.c_void_p(a.ctypes.data), 0, 0, a
         return C.c_void_p(a.ctypes.data), a.size, 0, a
+
+    def bgzf_compress(self, data, block_size=0, out=None):
+        """BlockCompressedOutputStream over `data` (bytes / numpy / torch tensor, host or device)
+        with the device deflate (hbam_bgzf_compress): the BGZF members, no terminator.  Returns
+        a numpy uint8 array, or writes into the device tensor `out` and returns its length."""
+        p, n, dev, keep = self._ptr(data)
+        bound = int(self.L.hbam_bgzf_bound(n, block_size))
+        if out is not None:
+            q, cap, odev, okeep = self._ptr(out)
+            r = self.L.hbam_bgzf_compress(self.h, p, dev, n, block_size, q, odev, cap)
+            if r < 0:
+                raise RuntimeError("hbam_bgzf_compress failed (%d): %s" % (r, self.last_error()))
+            return int(r)
+        buf = np.empty(max(bound, 1), np.uint8)
+        r = self.L.hbam_bgzf_compress(self.h, p, dev, n, block_size, C.c_void_p(buf.ctypes.data), 0, bound)
+        if r < 0:
+            raise RuntimeError("hbam_bgzf_compress failed (%d): %s" % (r, self.last_error()))
+        return buf[:r]
 
     def parse_header(self, data):
         p, n, dev, keep = self._ptr(data)

@@ -276,6 +276,21 @@ int64_t hbam_bgzf_block_index(hbam_ctx* ctx, const uint8_t* file, int on_device,
 int hbam_permute(hbam_ctx* ctx, const void* src, uint32_t elem_size, const uint32_t* perm,
                  uint64_t n, void* out);
 
+/* ---- BAM output ---------------------------------------------------------
+ * hbam_bgzf_compress: [htsjdk] BlockCompressedOutputStream under BAMRecordWriter
+ * (BAMRecordWriter.java:96-111, 113-124: the writer's stream, flushed without the EOF
+ * terminator) and SAMOutputPreparer.prepareForRecords (util/SAMOutputPreparer.java:58-95).
+ * Cuts [src, src + n) into blocks of block_size uncompressed bytes (0: 65280, at most 65280)
+ * and writes one BGZF member per block (DEFLATE on the device, CRC32, ISIZE) back to back
+ * into dst.  Returns the compressed length (>= 0) or a negative hbam status; dst_cap must be
+ * at least hbam_bgzf_bound(n, block_size).  The compressed bytes are not zlib's: parity is
+ * on the inflated bytes (any reader of BGZF gets src back).  No terminator is written: the
+ * caller appends the 28-byte EOF block where the reference does (Utils.mergeSAMInto,
+ * cli/Utils.java:351-353). */
+uint64_t hbam_bgzf_bound(uint64_t n, uint32_t block_size);
+int64_t hbam_bgzf_compress(hbam_ctx* ctx, const uint8_t* src, int src_on_device, uint64_t n,
+                           uint32_t block_size, uint8_t* dst, int dst_on_device, uint64_t dst_cap);
+
 /* ---- diagnostics (no reference counterpart) -----------------------------------------------
  * hbam_resolve_tokens: the LZ77 pass of the batched inflate (k_resolve) over ONE caller-built
  * token block: `io` (host, isize <= 65536 bytes) holds literal bytes with a 3-byte descriptor
