@@ -310,13 +310,13 @@ def main():
     alg = C_b + U_b
     achieved = alg / (inf_ms / 1e3) / 1e9
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "pmc_inflate.json")
+    pmc = os.path.join(ROOT, "profiles", "r02", "pmc_k_inflate_tokens.json")
     if os.path.exists(pmc):
         try:
             pj = json.load(open(pmc))
             if pj.get("comp_bytes") and abs(pj["comp_bytes"] - C_b) / C_b < 0.05 and \
                     pj.get("kernel") == "k_inflate_tokens" and pj.get("tree") == "round2":
-                traffic, traffic_src = pj.get("hbm_bytes_per_launch"), "profiles/pmc_inflate.json"
+                traffic, traffic_src = pj.get("hbm_bytes_per_launch"), "profiles/r02/pmc_k_inflate_tokens.json"
         except Exception:
             traffic = None
     result = {

@@ -1844,6 +1844,10 @@ extern "C" int hbam_prof_attach(void* dev) {
   unsigned long long* p = (unsigned long long*)dev;
   return hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_prof), &p, sizeof p) == hipSuccess ? 0 : -1;
 }
+extern "C" int hbam_prof_attach_deflate(void* dev) {
+  unsigned long long* p = (unsigned long long*)dev;
+  return hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_dfprof), &p, sizeof p) == hipSuccess ? 0 : -1;
+}
 extern "C" int hbam_prof_attach_trace(void* dev, unsigned int idx) {
   unsigned long long* p = (unsigned long long*)dev;
   if (hipMemcpyToSymbol(HIP_SYMBOL(hbam::g_gtrace_idx), &idx, sizeof idx) != hipSuccess) return -1;
@@ -1890,17 +1894,17 @@ extern "C" int64_t hbam_bgzf_compress(hbam_ctx* c, const uint8_t* src, int src_o
     const uint32_t k = (uint32_t)std::min<uint64_t>(DF_BATCH, nb - b0);
     const uint64_t off0 = b0 * bs;
     const uint64_t nn = std::min<uint64_t>(n - off0, (uint64_t)k * bs);
-    uint32_t *tok, *ntok, *freq, *crc, *csize;
+    uint32_t *tok, *ntok, *crc, *csize;
     uint8_t* slots;
     uint64_t* off;
     if ((rc = ensure(c, B_DF_TOK, (uint64_t)k * bs, &tok)) || (rc = ensure(c, B_DF_NTOK, k, &ntok)) ||
-        (rc = ensure(c, B_DF_FREQ, (uint64_t)k * DF_NSYM, &freq)) || (rc = ensure(c, B_DF_CRC, k, &crc)) ||
+        (rc = ensure(c, B_DF_CRC, k, &crc)) ||
         (rc = ensure(c, B_DF_SLOTS, (uint64_t)k * DF_SLOT, &slots)) || (rc = ensure(c, B_DF_CSIZE, k + 1, &csize)) ||
         (rc = ensure(c, B_DF_OFF, k + 1, &off)))
       return rc;
     k_crc_blocks<<<grid_for(k, 256), 256, 0, c->stream>>>(d + off0, nn, bs, k, crc);
-    k_lz77_tokens<<<k, DF_WG, 0, c->stream>>>(d + off0, nn, bs, k, tok, ntok, freq);
-    k_deflate_encode<<<k, DF_WG, 0, c->stream>>>(d + off0, nn, bs, k, tok, ntok, freq, crc, slots, csize);
+    k_lz77_tokens<<<k, DF_WG, 0, c->stream>>>(d + off0, nn, bs, k, tok, ntok);
+    k_deflate_encode<<<k, DF_WG, 0, c->stream>>>(d + off0, nn, bs, k, tok, ntok, crc, slots, csize);
     HIPCHK(c, hipGetLastError());
     uint64_t bytes = 0;
     if ((rc = scan_exclusive<uint32_t>(c, csize, k, off, &bytes))) return rc;

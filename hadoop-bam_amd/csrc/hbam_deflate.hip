@@ -8,13 +8,15 @@
 // DEFLATE stream is accepted by htsjdk's reader, so the compressor is free to be GPU-shaped.
 //
 //   k_lz77_tokens (one 256-thread workgroup per block): the block is staged in LDS; for every
-//     256-position chunk each thread finds the longest match at its position among the most
-//     recent earlier position with the same 4-byte hash (from earlier chunks) and the four
-//     previous positions (byte / short-period runs); wave 0 then walks the chunk greedily
-//     with readlane (the parse is serial, the data already in registers), emitting tokens
-//     to a per-block global buffer and symbol frequencies to LDS.
-//   k_deflate_encode (one 256-thread workgroup per block): length-limited Huffman codes from
-//     the frequencies (lit/len ≤ 15, distance ≤ 15, code-length code ≤ 7), the dynamic-block
+//     256-position chunk each thread probes (up to 16 bytes) the most recent earlier position
+//     with the same 4-byte hash (from earlier chunks) and the four previous positions (byte /
+//     short-period runs), extending a match the probe capped to its full length; the
+//     greedy parse of the chunk is then found by pointer jumping over the successor of each
+//     position (2^k-th successors, then the path from the entry marked level by level), and
+//     every thread writes its position's token at its rank.  Tokens go to a per-block global
+//     buffer.
+//   k_deflate_encode (one 256-thread workgroup per block): symbol frequencies from the
+//     tokens, length-limited Huffman codes (lit/len ≤ 15, distance ≤ 15, code-length code ≤ 7), the dynamic-block
 //     header, then every token's bit offset by a block-wide scan and its bits OR-ed into an
 //     LDS output image; a block that does not shrink is written as a stored block.  The
 //     BGZF member goes to a 64 KiB slot; a scan + copy packs the slots.
@@ -31,18 +33,21 @@ constexpr uint32_t DF_HBITS = 11;             // 2048-entry hash heads
 constexpr uint32_t DF_SLOT = 65536;           // BGZF member slot (BSIZE <= 65536)
 constexpr uint32_t DF_NSYM = 286 + 30;        // lit/len + distance frequencies per block
 constexpr uint32_t DF_WINDOW = 32768;
+constexpr uint32_t DF_PROBE = 16;             // match bytes verified per position in parallel
 
 __device__ __forceinline__ uint32_t df_hash(uint32_t w) { return (w * 2654435761u) >> (32 - DF_HBITS); }
 
 __device__ __forceinline__ uint32_t df_rd32(const uint8_t* s, uint32_t p) {
   return (uint32_t)s[p] | (uint32_t)s[p + 1] << 8 | (uint32_t)s[p + 2] << 16 | (uint32_t)s[p + 3] << 24;
 }
+// unaligned dword from LDS (the device runs in unaligned access mode, as k_resolve relies on)
+__device__ __forceinline__ uint32_t df_lds32(const uint8_t* s, uint32_t p) { return *(const uint32_t*)(s + p); }
 
 // length of the common prefix of s[a..] and s[p..], at most lim
 __device__ __forceinline__ uint32_t df_match(const uint8_t* s, uint32_t a, uint32_t p, uint32_t lim) {
   uint32_t l = 0;
   while (l + 4 <= lim) {
-    const uint32_t x = df_rd32(s, a + l) ^ df_rd32(s, p + l);
+    const uint32_t x = df_lds32(s, a + l) ^ df_lds32(s, p + l);
     if (x) return l + (__builtin_ctz(x) >> 3);
     l += 4;
   }
@@ -79,45 +84,67 @@ __device__ __forceinline__ void df_dist_code(uint32_t d, uint32_t& sym, uint32_t
   ev = x - ((2u + hb) << eb);
 }
 
+#ifdef HBAM_PROF
+__device__ unsigned long long* g_dfprof = nullptr;  // 8 u64 per block (tools/prof_deflate.py)
+#define DF_T() __builtin_amdgcn_s_memtime()
+#endif
 // token: literal = byte; match = 1<<31 | len<<16 | dist (dist <= 32768, len <= 258)
 __global__ __launch_bounds__(DF_WG) void k_lz77_tokens(const uint8_t* __restrict__ src, uint64_t n,
                                                        uint32_t bsize, uint32_t nblk,
                                                        uint32_t* __restrict__ tok,
-                                                       uint32_t* __restrict__ ntok,
-                                                       uint32_t* __restrict__ freq) {
+                                                       uint32_t* __restrict__ ntok) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[DF_MAXB + 288];
   __shared__ uint32_t s_head[1u << DF_HBITS];
   __shared__ uint32_t s_ml[DF_WG];
-  __shared__ uint32_t s_freq[DF_NSYM];
-  const uint32_t b = blockIdx.x, t = threadIdx.x, lane = t & 63u;
+  __shared__ uint16_t s_jmp[8][DF_WG];  // 2^k-th successor in the greedy parse
+  __shared__ uint32_t s_vis[8];         // token starts of the chunk
+  const uint32_t b = blockIdx.x, t = threadIdx.x;
   if (b >= nblk) return;
   const uint64_t start = (uint64_t)b * bsize;
   const uint32_t len = (uint32_t)((n - start) < bsize ? (n - start) : bsize);
-  for (uint32_t i = t; i < (DF_MAXB + 288) / 4; i += DF_WG) {
-    const uint32_t p = 4 * i;
-    uint32_t w = 0;
-    if (p + 4 <= len) {
-      w = df_rd32(src + start, p);  // byte loads: src has no alignment guarantee
-    } else {
-      for (uint32_t k = 0; k < 4; ++k)
-        if (p + k < len) w |= (uint32_t)src[start + p + k] << (8 * k);
+  const uint8_t* sb = src + start;
+  if (((uintptr_t)sb & 15u) == 0) {  // 16-byte loads (the caller's buffer is usually aligned)
+    for (uint32_t i = t; i < (DF_MAXB + 288) / 16; i += DF_WG) {
+      const uint32_t p = 16 * i;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (p + 16 <= len) {
+        v = *(const uint4*)(sb + p);
+      } else if (p < len) {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; p + k < len; ++k) w[k >> 2] |= (uint32_t)sb[p + k] << (8 * (k & 3u));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      ((uint4*)s_in)[i] = v;
     }
-    ((uint32_t*)s_in)[i] = w;
+  } else {
+    for (uint32_t i = t; i < (DF_MAXB + 288) / 4; i += DF_WG) {
+      const uint32_t p = 4 * i;
+      uint32_t w = 0;
+      for (uint32_t k = 0; k < 4; ++k)
+        if (p + k < len) w |= (uint32_t)sb[p + k] << (8 * k);
+      ((uint32_t*)s_in)[i] = w;
+    }
   }
   for (uint32_t i = t; i < (1u << DF_HBITS); i += DF_WG) s_head[i] = 0;
-  for (uint32_t i = t; i < DF_NSYM; i += DF_WG) s_freq[i] = 0;
   __syncthreads();
   uint32_t* out = tok + (uint64_t)b * bsize;
   uint32_t nxt = 0, nt = 0;  // parse position / tokens emitted (wave 0, uniform)
-  uint32_t tbuf = 0;         // wave 0: the next 64 tokens, one per lane
+#ifdef HBAM_PROF
+  uint64_t pt0 = DF_T(), p_match = 0, p_walk = 0, p_sync = 0, n_iter = 0, tq;
+#endif
   for (uint32_t c0 = 0; c0 < len; c0 += DF_WG) {
+#ifdef HBAM_PROF
+    const uint64_t tm0 = DF_T();
+#endif
     const uint32_t p = c0 + t;
     uint32_t best = 0;
     uint32_t h = 0;
     const bool has4 = p + 4 <= len;
     if (has4) {
-      const uint32_t lim = (len - p) < 258u ? (len - p) : 258u;
-      h = df_hash(df_rd32(s_in, p));
+      // lengths are found up to DF_PROBE bytes for every position; the parse extends the
+      // matches it takes (only those) to their full length
+      const uint32_t lim = (len - p) < DF_PROBE ? (len - p) : DF_PROBE;
+      h = df_hash(df_lds32(s_in, p));
       uint32_t bl = 0, bd = 0;
       // short periods first: runs of one byte and of short repeats are the commonest match
 #pragma unroll
@@ -141,60 +168,109 @@ __global__ __launch_bounds__(DF_WG) void k_lz77_tokens(const uint8_t* __restrict
           }
         }
       }
-      if (bl >= 4 || (bl == 3 && bd <= 64)) best = 0x80000000u | bl << 16 | bd;
-    }
-    s_ml[t] = best;
-    __syncthreads();
-    if (has4) atomicMax(&s_head[h], p + 1);  // most recent position of the hash, for later chunks
-    if (t < 64) {
-      // greedy parse of this chunk from nxt (uniform across wave 0; the chunk's match info is
-      // read into registers once and walked with readlane)
-      const uint32_t m0 = s_ml[lane], m1 = s_ml[64 + lane], m2 = s_ml[128 + lane], m3 = s_ml[192 + lane];
-      const uint32_t cend = (c0 + DF_WG < len) ? c0 + DF_WG : len;
-      while (nxt < cend) {
-        const uint32_t r = nxt - c0;
-        const uint32_t q = r & 63u;
-        uint32_t m;
-        if (r < 64) m = __builtin_amdgcn_readlane(m0, q);
-        else if (r < 128) m = __builtin_amdgcn_readlane(m1, q);
-        else if (r < 192) m = __builtin_amdgcn_readlane(m2, q);
-        else m = __builtin_amdgcn_readlane(m3, q);
-        uint32_t tk, step;
-        if (m) {
-          tk = m;
-          step = (m >> 16) & 0x1ffu;
-        } else {
-          tk = s_in[nxt];
-          step = 1;
+      if (bl >= 4 || (bl == 3 && bd <= 64)) {
+        if (bl == DF_PROBE) {  // the probe capped it: this position's full length (<= 258)
+          const uint32_t full = (len - p) < 258u ? (len - p) : 258u;
+          bl += df_match(s_in, p - bd + DF_PROBE, p + DF_PROBE, full - DF_PROBE);
         }
-        if (lane == (nt & 63u)) tbuf = tk;
-        if (lane == 0) {
-          if (m) {
-            uint32_t sy, eb, ev;
-            df_len_code(step, sy, eb, ev);
-            atomicAdd(&s_freq[sy], 1u);
-            df_dist_code(m & 0xffffu, sy, eb, ev);
-            atomicAdd(&s_freq[286 + sy], 1u);
-          } else {
-            atomicAdd(&s_freq[tk], 1u);
-          }
-        }
-        ++nt;
-        if ((nt & 63u) == 0) out[nt - 64 + lane] = tbuf;
-        nxt += step;
+        best = 0x80000000u | bl << 16 | bd;
       }
     }
+    s_ml[t] = best;
+#ifdef HBAM_PROF
+    tq = DF_T();
+    p_match += tq - tm0;
+#endif
+    // successor of each position in the greedy parse (256 = past the chunk)
+    const uint32_t cend = (c0 + DF_WG < len) ? c0 + DF_WG : len;
+    {
+      const uint32_t step = best ? (best >> 16) & 0x1ffu : 1u;
+      const uint32_t nx = t + step;
+      s_jmp[0][t] = (uint16_t)((p < cend && c0 + nx < cend) ? nx : DF_WG);
+    }
+    if (t < 8) s_vis[t] = 0;
+    __syncthreads();
+#ifdef HBAM_PROF
+    {
+      const uint64_t t2 = DF_T();
+      p_sync += t2 - tq;
+      tq = t2;
+    }
+#endif
+    if (has4) atomicMax(&s_head[h], p + 1);  // most recent position of the hash, for later chunks
+    // Greedy parse of the chunk from nxt by pointer jumping: jmp[k][i] = the 2^k-th successor
+    // of i; then the token starts = steps 0.. of the path from nxt, found from the most
+    // significant jump down (after level k the set holds every step that is a multiple of
+    // 2^k), then every thread emits its position's token at its rank among the starts.
+#pragma unroll 1
+    for (uint32_t k = 1; k < 8; ++k) {
+      const uint32_t j = s_jmp[k - 1][t];
+      s_jmp[k][t] = j < DF_WG ? s_jmp[k - 1][j] : (uint16_t)DF_WG;
+      __syncthreads();
+    }
+    const uint32_t e = nxt - c0;  // nxt is uniform: every thread tracks it
+    if (nxt < cend) {
+      if (t == 0) s_vis[e >> 5] = 1u << (e & 31u);
+      __syncthreads();
+#pragma unroll 1
+      for (int k = 7; k >= 0; --k) {
+        if ((s_vis[t >> 5] >> (t & 31u)) & 1u) {
+          const uint32_t j = s_jmp[k][t];
+          if (j < DF_WG) atomicOr(&s_vis[j >> 5], 1u << (j & 31u));
+        }
+        __syncthreads();
+      }
+      // rank of each start: whole words before + bits below in its word
+      const uint32_t w = t >> 5, bit = t & 31u;
+      uint32_t before = 0, total = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 8; ++q) {
+        const uint32_t c = (uint32_t)__popc(s_vis[q]);
+        before += q < w ? c : 0u;
+        total += c;
+      }
+      const uint32_t vw = s_vis[w];
+      if ((vw >> bit) & 1u) {
+        before += (uint32_t)__popc(vw & ((1u << bit) - 1u));
+        out[nt + before] = best ? best : (uint32_t)s_in[p];
+      }
+      // the last start's successor is where the next chunk's parse begins
+      uint32_t last = 0;
+#pragma unroll
+      for (int q = 7; q >= 0; --q) {
+        if (s_vis[q]) {
+          last = 32u * (uint32_t)q + 31u - (uint32_t)__clz(s_vis[q]);
+          break;
+        }
+      }
+      const uint32_t lm = s_ml[last];
+      nt += total;
+      nxt = c0 + last + (lm ? (lm >> 16) & 0x1ffu : 1u);
+#ifdef HBAM_PROF
+      n_iter += total;
+#endif
+    }
+#ifdef HBAM_PROF
+    {
+      const uint64_t t2 = DF_T();
+      p_walk += t2 - tq;
+      tq = t2;
+    }
+#endif
     __syncthreads();
   }
-  if (t < 64) {
-    if (lane < (nt & 63u)) out[(nt & ~63u) + lane] = tbuf;
-    if (t == 0) {
-      ntok[b] = nt;
-      atomicAdd(&s_freq[256], 1u);  // end of block
-    }
+  if (t == 0) ntok[b] = nt;
+#ifdef HBAM_PROF
+  if (g_dfprof && t == 0) {
+    unsigned long long* g = g_dfprof + 8 * (uint64_t)b;
+    g[0] = DF_T() - pt0;
+    g[1] = p_walk;
+    g[2] = p_sync;
+    g[3] = n_iter;
+    g[4] = nt;
+    g[5] = p_match;
   }
-  __syncthreads();
-  for (uint32_t i = t; i < DF_NSYM; i += DF_WG) freq[(uint64_t)b * DF_NSYM + i] = s_freq[i];
+#endif
 }
 
 // ---- Huffman code lengths (one thread): Huffman tree by two queues over the symbols sorted
@@ -311,7 +387,6 @@ __global__ __launch_bounds__(DF_WG) void k_deflate_encode(const uint8_t* __restr
                                                           uint32_t bsize, uint32_t nblk,
                                                           const uint32_t* __restrict__ tok,
                                                           const uint32_t* __restrict__ ntok,
-                                                          const uint32_t* __restrict__ freq,
                                                           const uint32_t* __restrict__ crc,
                                                           uint8_t* __restrict__ slots,
                                                           uint32_t* __restrict__ csize) {
@@ -332,8 +407,23 @@ __global__ __launch_bounds__(DF_WG) void k_deflate_encode(const uint8_t* __restr
   const uint64_t start = (uint64_t)b * bsize;
   const uint32_t len = (uint32_t)((n - start) < bsize ? (n - start) : bsize);
   const uint32_t nt = ntok[b];
-  for (uint32_t i = t; i < DF_NSYM; i += DF_WG) s_f[i] = freq[(uint64_t)b * DF_NSYM + i];
+  const uint32_t* tk = tok + (uint64_t)b * bsize;
+  for (uint32_t i = t; i < DF_NSYM; i += DF_WG) s_f[i] = 0;
   for (uint32_t i = t; i < DF_OUTW; i += DF_WG) s_out[i] = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < nt; i += DF_WG) {  // symbol frequencies of the block's tokens
+    const uint32_t x = tk[i];
+    if (x & 0x80000000u) {
+      uint32_t sy, eb, ev;
+      df_len_code((x >> 16) & 0x1ffu, sy, eb, ev);
+      atomicAdd(&s_f[sy], 1u);
+      df_dist_code(x & 0xffffu, sy, eb, ev);
+      atomicAdd(&s_f[286 + sy], 1u);
+    } else {
+      atomicAdd(&s_f[x], 1u);
+    }
+  }
+  if (t == 0) atomicAdd(&s_f[256], 1u);  // end of block
   __syncthreads();
   if (t == 0) {
     // a complete lit/len code needs two symbols; the end-of-block symbol is always used
@@ -432,7 +522,6 @@ __global__ __launch_bounds__(DF_WG) void k_deflate_encode(const uint8_t* __restr
   }
   __syncthreads();
   // tokens: each round 256 tokens, bit offsets by a block-wide exclusive scan
-  const uint32_t* tk = tok + (uint64_t)b * bsize;
   uint32_t base = s_bits;
   bool overflow = false;
   for (uint32_t r0 = 0; r0 < nt; r0 += DF_WG) {
@@ -540,14 +629,22 @@ __global__ void k_pack_members(const uint8_t* __restrict__ slots, const uint32_t
   for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) d[i] = s[i];
 }
 
-// CRC-32 of each uncompressed block (blocks of bsize over src), one thread per block
+// CRC-32 of each uncompressed block (blocks of bsize over src), one thread per block:
+// slice-by-4 tables in LDS, 16-byte loads when the block is 16-aligned
 __global__ __launch_bounds__(256) void k_crc_blocks(const uint8_t* __restrict__ src, uint64_t n, uint32_t bsize,
                                                     uint32_t nblk, uint32_t* __restrict__ crc_out) {
-  __shared__ uint32_t T[256];
+  __shared__ uint32_t T[4][256];
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = (c & 1u) ? 0xedb88320u ^ (c >> 1) : c >> 1;
-    T[i] = c;
+    T[0][i] = c;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t c = T[0][i];
+    c = T[0][c & 0xff] ^ (c >> 8); T[1][i] = c;
+    c = T[0][c & 0xff] ^ (c >> 8); T[2][i] = c;
+    c = T[0][c & 0xff] ^ (c >> 8); T[3][i] = c;
   }
   __syncthreads();
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -555,8 +652,23 @@ __global__ __launch_bounds__(256) void k_crc_blocks(const uint8_t* __restrict__ 
   const uint64_t start = (uint64_t)b * bsize;
   const uint32_t len = (uint32_t)((n - start) < bsize ? (n - start) : bsize);
   const uint8_t* p = src + start;
-  uint32_t c = 0xffffffffu;
-  for (uint32_t i = 0; i < len; ++i) c = T[(c ^ p[i]) & 0xffu] ^ (c >> 8);
+  uint32_t c = 0xffffffffu, i = 0;
+  auto word = [&](uint32_t w) {
+    c ^= w;
+    c = T[3][c & 0xff] ^ T[2][(c >> 8) & 0xff] ^ T[1][(c >> 16) & 0xff] ^ T[0][c >> 24];
+  };
+  if (((uintptr_t)p & 15u) == 0) {
+    uint4 v = len >= 16 ? *(const uint4*)p : make_uint4(0, 0, 0, 0);
+    for (; i + 16 <= len; i += 16) {
+      const uint4 cur = v;
+      if (i + 32 <= len) v = *(const uint4*)(p + i + 16);  // next quad in flight
+      word(cur.x);
+      word(cur.y);
+      word(cur.z);
+      word(cur.w);
+    }
+  }
+  for (; i < len; ++i) c = T[0][(c ^ p[i]) & 0xffu] ^ (c >> 8);
   crc_out[b] = ~c;
 }
 

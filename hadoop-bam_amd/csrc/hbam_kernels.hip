@@ -364,16 +364,26 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     p_desc += q1 - q0;
     n_m += total;
 #endif
-    // ---- pre matches: all sources final (those older than the window were written back
-    // two stretches ago; drain this wave's stores before reading them)
+    // ---- pre matches: all sources final.  LDS holds block offsets from s0 - RS_W - a0 (the
+    // previous stretch's write-back region); a source older than that is read from ubuf
+    // (stretches <= k-2, written back at least one iteration ago; the drain below makes that
+    // explicit), and a source that straddles the boundary is copied in two parts.
+#ifndef HBAM_RS_NODRAIN  // A/B at 10 GB without the drain: 58.8 vs 58.6 ms, so it stays
     if (s0 >= RS_W) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    const uint32_t lds_from = s0 - RS_W - a0;  // block offset of LDS index 0 (when s0 >= RS_W)
     for (uint32_t j = lane; j < npre; j += 64) {
       const uint64_t rec = s_rec[j];
       const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
                      dist = (uint32_t)(rec >> 32) & 0xffffu;
       const uint32_t src = p - dist;
-      if (src + RS_W >= s0) rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
-      else rs_copy_glb(s_buf, lbase + p, len, ubuf + base + src);
+      if (src + RS_W + a0 >= s0) {
+        rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
+      } else {  // dist > RS_W >= 258 >= len: no overlap with the destination
+        const uint32_t gl = (lds_from - src) < len ? (lds_from - src) : len;
+        rs_copy_glb(s_buf, lbase + p, gl, ubuf + base + src);
+        if (gl < len) rs_copy_lds(s_buf, lbase + p + gl, len - gl, dist, s_sel);
+      }
     }
 #ifdef HBAM_PROF
     p_pre += PROF_CLK() - q1;
@@ -466,7 +476,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
       uint32_t jj = 0;
       for (uint32_t t = 0; t < n && !tail_bad; ++t) {
         const uint32_t x = p - d + jj;
-        s_buf[lbase + p + t] = (x + RS_W >= s0) ? s_buf[lbase + x] : ubuf[base + x];
+        s_buf[lbase + p + t] = (x + RS_W + a0 >= s0) ? s_buf[lbase + x] : ubuf[base + x];
         jj = (jj + 1u == d) ? 0u : jj + 1u;
       }
     }
