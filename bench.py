@@ -199,15 +199,22 @@ def main():
     dist = None
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # RCCL between GPUs; HBAM_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks on
+    # one GPU (host-staged collectives), which is how it is tested on the one-GPU pool
+    backend = os.environ.get("HBAM_BENCH_BACKEND", "nccl")
+    cdev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from hadoop_bam import _lib
     ctx = _lib.Context(local)
 
     buf, own_len, off, file_len, n_own = make_shard(int(args.size), args.seed, rank, world,
-                                                    threads, dist, dev)
+                                                    threads, dist, cdev)
     dcomp = torch.empty(len(buf) + 64, dtype=torch.uint8, device=dev)
     dcomp[len(buf):].zero_()
     dcomp[:len(buf)].copy_(torch.from_numpy(buf), non_blocking=False)
@@ -260,7 +267,7 @@ def main():
                                   C.c_void_p(perm.data_ptr()), k, C.c_void_p(head.data_ptr())) == 0
         overlap = int(((head.cpu() >> 16) == off).sum())
     tot = torch.tensor([elapsed, float(ubytes), float(n_rec), float(own_len), float(n_own),
-                        float(overlap)], dtype=torch.float64, device=dev)
+                        float(overlap)], dtype=torch.float64, device=cdev)
     if dist:
         mx = tot.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
