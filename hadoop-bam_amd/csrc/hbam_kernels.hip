@@ -397,37 +397,42 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     if (nord) {
       for (uint32_t w = lane; w < RS_PW; w += 64) s_pend[w] = 0u;
       rs_wave_sync();
-      // this lane's matches lane + 64 t (s_rec, read back each round: registers for six
+      // this lane's matches lane + 64 t: the first in registers (most stretches have fewer
+      // than 64 ordered matches), the rest read back from s_rec each round (registers for six
       // slots would cost the kernel half its occupancy)
       const uint32_t mine = nord > lane ? (nord - lane + 63u) / 64u : 0u;
       uint32_t live = mine >= 32u ? ~0u : (1u << mine) - 1u;
+      const uint64_t rec0 = mine ? s_rec[RS_MAXM - 1 - lane] : 0ull;
+      if (mine) rs_bits(s_pend, ((uint32_t)rec0 & 0xffffu) - s0, (uint32_t)(rec0 >> 16) & 0xffffu, true);
 #pragma unroll 1
-      for (uint32_t t = 0; t < mine; ++t) {
+      for (uint32_t t = 1; t < mine; ++t) {
         const uint64_t rec = s_rec[RS_MAXM - 1 - (lane + 64u * t)];
         rs_bits(s_pend, ((uint32_t)rec & 0xffffu) - s0, (uint32_t)(rec >> 16) & 0xffffu, true);
       }
-      rs_wave_sync();
+      rs_lds_order();
+      auto is_ready = [&](uint64_t rec) {
+        const uint32_t p = (uint32_t)rec & 0xffffu, dist = (uint32_t)(rec >> 32) & 0xffffu;
+        const uint32_t e = (uint32_t)(rec >> 48);
+        const uint32_t a = p - dist;
+        const uint32_t lo = a > s0 ? a - s0 : 0u;  // bytes before the stretch are final
+        return e <= s0 + lo || !rs_any_bit(s_pend, lo, e - s0);
+      };
+      auto run = [&](uint64_t rec) {
+        const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
+                       dist = (uint32_t)(rec >> 32) & 0xffffu;
+        rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
+        rs_bits(s_pend, p - s0, len, false);
+      };
       for (;;) {
-        uint32_t ready = 0;
+        uint32_t ready = (live & 1u) && is_ready(rec0) ? 1u : 0u;
 #pragma unroll 1
-        for (uint32_t t = 0; t < mine; ++t) {
-          if (!(live >> t & 1u)) continue;
-          const uint64_t rec = s_rec[RS_MAXM - 1 - (lane + 64u * t)];
-          const uint32_t p = (uint32_t)rec & 0xffffu, dist = (uint32_t)(rec >> 32) & 0xffffu;
-          const uint32_t e = (uint32_t)(rec >> 48);
-          const uint32_t a = p - dist;
-          const uint32_t lo = a > s0 ? a - s0 : 0u;  // bytes before the stretch are final
-          if (e <= s0 + lo || !rs_any_bit(s_pend, lo, e - s0)) ready |= 1u << t;
-        }
+        for (uint32_t t = 1; t < mine; ++t)
+          if ((live >> t & 1u) && is_ready(s_rec[RS_MAXM - 1 - (lane + 64u * t)])) ready |= 1u << t;
+        rs_lds_order();
+        if (ready & 1u) run(rec0);
 #pragma unroll 1
-        for (uint32_t t = 0; t < mine; ++t) {
-          if (!(ready >> t & 1u)) continue;
-          const uint64_t rec = s_rec[RS_MAXM - 1 - (lane + 64u * t)];
-          const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
-                         dist = (uint32_t)(rec >> 32) & 0xffffu;
-          rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
-          rs_bits(s_pend, p - s0, len, false);
-        }
+        for (uint32_t t = 1; t < mine; ++t)
+          if (ready >> t & 1u) run(s_rec[RS_MAXM - 1 - (lane + 64u * t)]);
         live &= ~ready;
 #ifdef HBAM_PROF
         ++n_bat;
@@ -437,7 +442,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
           if (lane == 0) status[b] = INF_DATA;
           return;
         }
-        rs_wave_sync();
+        rs_lds_order();
       }
     }
 #else

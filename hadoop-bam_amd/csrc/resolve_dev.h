@@ -47,6 +47,12 @@ __device__ __forceinline__ void rs_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   __builtin_amdgcn_wave_barrier();
 }
+// Between the phases of a dataflow round only program order matters: a wave's LDS
+// instructions execute in issue order, so a compiler barrier is enough (no lgkmcnt drain).
+__device__ __forceinline__ void rs_lds_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // set / clear bits [x, x + n) of an LDS bitmap (other lanes touch the same words: atomics)
 __device__ __forceinline__ void rs_bits(uint32_t* bm, uint32_t x, uint32_t n, bool set) {
