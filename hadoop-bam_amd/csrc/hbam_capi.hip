@@ -127,6 +127,29 @@ enum BufId {
   B_DF_CSIZE,
   B_DF_OFF,
   B_DF_DST,
+  // read-name / CIGAR keyed consumers (hbam_consumers.hip)
+  B_F4_CNT,
+  B_F4_OFF,
+  B_F4_ERR,
+  B_F4_KEY,
+  B_F4_BEG,
+  B_F4_END,
+  B_F4_REV,
+  B_F4_REC,
+  B_F4_NKEY,
+  B_F4_NP,
+  B_F4_NTMP,
+  B_F4_MM,
+  B_F4_PERM,
+  B_F4_GST,
+  B_F4_GCNT,
+  B_F4_GOUT,
+  B_F4_SRC,
+  B_F4_MATE,
+  B_F4_ROLE,
+  B_F4_LENS,
+  B_F4_OOFF,
+  B_F4_PAY,
   B_COUNT_ALL
 };
 
@@ -530,6 +553,13 @@ int hbam_upload(hbam_ctx* c, const uint8_t* host, uint64_t len, uint8_t** dev_ou
   if (len) HIPCHK(c, hipMemcpyAsync(d, host, len, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   *dev_out = d;
+  return HBAM_OK;
+}
+
+int hbam_download(hbam_ctx* c, const void* dev, uint64_t bytes, void* host) {
+  if (!c || (bytes && (!dev || !host))) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, copy_sync(c, host, dev, bytes, hipMemcpyDeviceToHost));
   return HBAM_OK;
 }
 
@@ -1931,3 +1961,5 @@ extern "C" int64_t hbam_bgzf_compress(hbam_ctx* c, const uint8_t* src, int src_o
   c->timing.n_blocks = nb;
   return (int64_t)out_total;
 }
+
+#include "hbam_consumers.hip"

@@ -26,6 +26,7 @@ HBAM_EUNSUPPORTED = -9
 HBAM_EDEVICE = -10
 HBAM_EINVAL = -11
 HBAM_EMORE = -12
+HBAM_EINDEX = -13
 
 CODE_NAMES = {
     HBAM_OK: "OK", HBAM_EIO: "IOException", HBAM_ETRUNC: "FileTruncatedException",
@@ -33,7 +34,7 @@ CODE_NAMES = {
     HBAM_EEOF: "RuntimeEOFException", HBAM_EREFID: "IllegalArgumentException",
     HBAM_EDATA: "RuntimeException(DataFormatException)", HBAM_ENOMEM: "OutOfMemory",
     HBAM_EUNSUPPORTED: "Unsupported", HBAM_EDEVICE: "DeviceError", HBAM_EINVAL: "InvalidArgument",
-    HBAM_EMORE: "NeedMoreData",
+    HBAM_EMORE: "NeedMoreData", HBAM_EINDEX: "IndexOutOfBoundsException",
 }
 
 # every entry point include/hbam.h declares (checked by tests/test_abi.py)
@@ -47,6 +48,7 @@ EXPORTS = [
     "hbam_bgzf_block_index", "hbam_resolve_tokens", "hbam_split_open", "hbam_split_next",
     "hbam_split_stats", "hbam_split_close", "hbam_device_alloc", "hbam_sort_split",
     "hbam_sort_partition", "hbam_sort_received", "hbam_bgzf_bound", "hbam_bgzf_compress",
+    "hbam_summarize_ranges", "hbam_name_order", "hbam_fixmate", "hbam_download",
 ]
 
 
@@ -81,6 +83,17 @@ class SortedRunC(C.Structure):
     _fields_ = [("n", C.c_uint64), ("payload_bytes", C.c_uint64), ("key", C.c_void_p),
                 ("voffset", C.c_void_p), ("block_size", C.c_void_p), ("offsets", C.c_void_p),
                 ("payload", C.c_void_p)]
+
+
+class RangesC(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("status", C.c_int32), ("pad", C.c_int32), ("key", C.c_void_p),
+                ("beg", C.c_void_p), ("end", C.c_void_p), ("rev", C.c_void_p), ("record", C.c_void_p)]
+
+
+class FixmateRunC(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("payload_bytes", C.c_uint64), ("n_groups", C.c_uint64),
+                ("status", C.c_int32), ("pad", C.c_int32), ("src", C.c_void_p), ("mate", C.c_void_p),
+                ("offsets", C.c_void_p), ("payload", C.c_void_p)]
 
 
 _u8p = C.POINTER(C.c_uint8)
@@ -132,6 +145,7 @@ def load(path=None):
         "hbam_get_timing": (C.c_int, [vp, C.POINTER(Timing)]),
         "hbam_upload": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(vp)]),
         "hbam_device_free": (C.c_int, [vp, vp]),
+        "hbam_download": (C.c_int, [vp, vp, C.c_uint64, vp]),
         "hbam_parse_header": (C.c_int, [vp, vp, C.c_int, C.c_uint64, C.POINTER(Header)]),
         "hbam_scan_blocks": (C.c_int, [vp, vp, C.c_int, C.c_uint64, C.c_uint64,
                                        C.POINTER(Block), C.c_uint64, C.POINTER(C.c_uint64)]),
@@ -169,6 +183,9 @@ def load(path=None):
         "hbam_sort_partition": (C.c_int, [vp, C.POINTER(SortedRunC), vp, C.c_uint32, vp, vp]),
         "hbam_sort_received": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, C.POINTER(SortedRunC)]),
         "hbam_bgzf_bound": (C.c_uint64, [C.c_uint64, C.c_uint32]),
+        "hbam_summarize_ranges": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(RangesC)]),
+        "hbam_name_order": (C.c_int, [vp, vp, vp, C.c_uint64, vp]),
+        "hbam_fixmate": (C.c_int, [vp, vp, vp, C.c_uint64, C.POINTER(FixmateRunC)]),
         "hbam_bgzf_compress": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int,
                                            C.c_uint64]),
     }
@@ -451,3 +468,45 @@ class Context:
         if r < 0:
             return int(r), None
         return 0, out[:r]
+
+    # ---- read-name / CIGAR keyed consumers --------------------------------
+    def _d2h(self, ptr, n, dtype):
+        """Copy n elements of a device array (context-owned) to a numpy array."""
+        out = np.empty(n, dtype)
+        if n:
+            rc = self.L.hbam_download(self.h, C.c_void_p(ptr), out.nbytes, C.c_void_p(out.ctypes.data))
+            if rc:
+                raise RuntimeError("hbam_download failed (%d): %s" % (rc, self.last_error()))
+        return out
+
+    def summarize_ranges(self, dcols):
+        """SummarizeRecordReader's ranges over device columns (hbam_summarize_ranges) -> dict of
+        numpy arrays + status."""
+        r = RangesC()
+        rc = self.L.hbam_summarize_ranges(self.h, C.byref(dcols), C.byref(r))
+        if rc:
+            raise RuntimeError("hbam_summarize_ranges failed (%d): %s" % (rc, self.last_error()))
+        n = int(r.n)
+        return dict(key=self._d2h(r.key, n, np.int64), beg=self._d2h(r.beg, n, np.int32),
+                    end=self._d2h(r.end, n, np.int32), rev=self._d2h(r.rev, n, np.uint8),
+                    record=self._d2h(r.record, n, np.uint32), status=int(r.status))
+
+    def name_order(self, ubuf_ptr, rec_off_ptr, n, perm_ptr):
+        rc = self.L.hbam_name_order(self.h, C.c_void_p(ubuf_ptr), C.c_void_p(rec_off_ptr), n,
+                                    C.c_void_p(perm_ptr))
+        if rc:
+            raise RuntimeError("hbam_name_order failed (%d): %s" % (rc, self.last_error()))
+
+    def fixmate(self, ubuf_ptr, rec_off_ptr, n):
+        """FixMateReducer over the name shuffle of n device records -> host dict(payload,
+        offsets, src, mate, n_groups, status)."""
+        r = FixmateRunC()
+        rc = self.L.hbam_fixmate(self.h, C.c_void_p(ubuf_ptr), C.c_void_p(rec_off_ptr), n, C.byref(r))
+        if rc:
+            raise RuntimeError("hbam_fixmate failed (%d): %s" % (rc, self.last_error()))
+        k = int(r.n)
+        return dict(payload=self._d2h(r.payload, int(r.payload_bytes), np.uint8),
+                    offsets=self._d2h(r.offsets, k + 1, np.uint64) if k else np.zeros(1, np.uint64),
+                    src=self._d2h(r.src, k, np.uint32), mate=self._d2h(r.mate, k, np.uint32),
+                    n_groups=int(r.n_groups), status=int(r.status))
+

@@ -14,6 +14,7 @@
  *   HBAM_EEOF         htsjdk.samtools.util.RuntimeEOFException
  *   HBAM_EREFID       IllegalArgumentException (reference index not in dictionary)
  *   HBAM_EDATA        RuntimeException(java.util.zip.DataFormatException)
+ *   HBAM_EINDEX       IndexOutOfBoundsException
  *
  * Library-specific codes (no reference counterpart): HBAM_ENOMEM, HBAM_EUNSUPPORTED
  * (BGZF block with ISIZE > 65536), HBAM_EDEVICE (HIP error), HBAM_EINVAL, HBAM_EMORE
@@ -46,6 +47,7 @@ extern "C" {
 #define HBAM_EDEVICE (-10)
 #define HBAM_EINVAL (-11)
 #define HBAM_EMORE (-12)
+#define HBAM_EINDEX (-13) /* IndexOutOfBoundsException (Summarize.java:715 on a record without a range) */
 
 typedef struct hbam_ctx hbam_ctx;
 
@@ -133,6 +135,9 @@ int hbam_get_timing(const hbam_ctx* ctx, hbam_timing* out);
 /* ---- device staging (the Java shim maps HDFS bytes into pinned buffers) ---------- */
 int hbam_upload(hbam_ctx* ctx, const uint8_t* host, uint64_t len, uint8_t** dev_out);
 int hbam_device_free(hbam_ctx* ctx, uint8_t* dev);
+/* copy `bytes` of library-owned device memory (e.g. an f-4 output) to host memory, ordered after
+ * the context's work */
+int hbam_download(hbam_ctx* ctx, const void* dev, uint64_t bytes, void* host);
 
 /* ---- SAMHeaderReader.readSAMHeaderFrom (util/SAMHeaderReader.java:53-72) ----------
  * `file` holds the start of the BAM file (host or device per `on_device`). */
@@ -290,6 +295,53 @@ int hbam_permute(hbam_ctx* ctx, const void* src, uint32_t elem_size, const uint3
 uint64_t hbam_bgzf_bound(uint64_t n, uint32_t block_size);
 int64_t hbam_bgzf_compress(hbam_ctx* ctx, const uint8_t* src, int src_on_device, uint64_t n,
                            uint32_t block_size, uint8_t* dst, int dst_on_device, uint64_t dst_cap);
+
+/* ---- read-name / CIGAR keyed consumers -------------------------------------
+ * Output buffers are device memory owned by the context, valid until the next call of the same
+ * entry point on that context. */
+/* SummarizeRecordReader (cli/plugins/chipster/Summarize.java:664-755) over a decoded split (dv:
+ * device columns of hbam_decode_split / hbam_split_next): for every record that is mapped, placed
+ * and has getAlignmentStart() >= 0 (:708-709), the reference ranges of its CIGAR (parseCIGAR
+ * :719-755; M/=/X runs, D/N skip) in order, each with the LongWritable key nextKeyValue sets
+ * (:696-699, :714-715: getKey0(refIdx, centre of mass), then the high word kept).  status: the
+ * exception nextKeyValue raises after the n ranges — the split's own (dv->status), HBAM_EREFID
+ * (IllegalArgumentException: a CIGAR op code > 8) or HBAM_EINDEX (a record without a range). */
+typedef struct hbam_ranges {
+  uint64_t n;
+  int32_t status;
+  int32_t pad;
+  int64_t* key;
+  int32_t* beg;      /* Range.beg: 1-based, inclusive */
+  int32_t* end;      /* Range.end: inclusive */
+  uint8_t* rev;      /* Range.reverseStrand */
+  uint32_t* record;  /* the record (index in dv) the range comes from */
+} hbam_ranges;
+int hbam_summarize_ranges(hbam_ctx* ctx, const hbam_columns* dv, hbam_ranges* out);
+/* FixMateMapper's shuffle (cli/plugins/FixMate.java:209-221): perm (device, u32[n]) = the n records
+ * at ubuf + rec_off[i] (device; a decoded split's ubuf/rec_off or a packed payload and its offsets)
+ * in the order of their Text(getReadName()) keys — unsigned lexicographic, proper prefix first —
+ * ties in input order (the reference leaves them unspecified). */
+int hbam_name_order(hbam_ctx* ctx, const uint8_t* ubuf, const uint64_t* rec_off, uint64_t n, uint32_t* perm);
+/* FixMateReducer (FixMate.java:225-277) over that shuffle order, without the combiner: the
+ * reducer's writes in order.  Output k is SAMRecordWritable.write of input record src[k] — as read
+ * (mate[k] == 0xffffffff: a secondary, or an unpaired primary) or after SamPairUtil.setMateInfo with
+ * record mate[k] (mate fields, flags 0x8/0x20, TLEN, MQ set / MC removed, re-encoded).  The
+ * reducer's quirk is kept: a primary followed only by secondaries is mated with the last of them,
+ * which is written twice.  status: HBAM_EFORMAT when a mated record's attributes do not parse (the
+ * job fails at output n). */
+typedef struct hbam_fixmate_run {
+  uint64_t n;
+  uint64_t payload_bytes;
+  uint64_t n_groups;   /* reduce groups (distinct read names) */
+  int32_t status;
+  int32_t pad;
+  uint32_t* src;
+  uint32_t* mate;
+  uint64_t* offsets;   /* n+1 */
+  uint8_t* payload;
+} hbam_fixmate_run;
+int hbam_fixmate(hbam_ctx* ctx, const uint8_t* ubuf, const uint64_t* rec_off, uint64_t n,
+                 hbam_fixmate_run* out);
 
 /* ---- diagnostics (no reference counterpart) -----------------------------------------------
  * hbam_resolve_tokens: the LZ77 pass of the batched inflate (k_resolve) over ONE caller-built

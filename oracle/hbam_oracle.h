@@ -148,6 +148,21 @@ int or_read_split_cols(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_
                        int check_crc, int keep_var, or_cols* out);
 void or_cols_free(or_cols* c);
 
+
+/* ---- read-name / CIGAR keyed consumers (hbam_oracle_f4.c) ----------------
+ * Records are SAMRecordWritable payloads (block_size + record) at pay + off[i]. */
+/* SummarizeRecordReader (cli/plugins/chipster/Summarize.java:664-755): ranges of every mapped
+ * record; returns the count, *status = the exception raised after them (split_status, OR_EREFID
+ * for a CIGAR op > 8, -13 IndexOutOfBoundsException for a record without a range). */
+int64_t or_summarize_ranges(const uint8_t* pay, const uint64_t* off, uint64_t n, int32_t split_status,
+                            int64_t* key, int32_t* beg, int32_t* end, uint8_t* rev, uint32_t* rec,
+                            uint64_t cap, int32_t* status);
+/* FixMateMapper's shuffle order: (Text(readName), input order) */
+void or_name_order(const uint8_t* pay, const uint64_t* off, uint64_t n, uint32_t* perm);
+/* FixMateReducer (FixMate.java:230-277) over the shuffle order: the reducer's writes */
+int64_t or_fixmate(const uint8_t* pay, const uint64_t* off, uint64_t n, uint8_t* out_pay, uint64_t* out_off,
+                   uint32_t* out_src, uint64_t cap, uint64_t pay_cap, int32_t* status);
+
 #ifdef __cplusplus
 }
 #endif

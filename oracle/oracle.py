@@ -61,6 +61,15 @@ def lib():
                                          C.POINTER(OrCols)]
         L.or_cols_free.restype = None
         L.or_cols_free.argtypes = [C.POINTER(OrCols)]
+        vp = C.c_void_p
+        L.or_summarize_ranges.restype = C.c_int64
+        L.or_summarize_ranges.argtypes = [vp, vp, C.c_uint64, C.c_int32, vp, vp, vp, vp, vp,
+                                          C.c_uint64, C.POINTER(C.c_int32)]
+        L.or_name_order.restype = None
+        L.or_name_order.argtypes = [vp, vp, C.c_uint64, vp]
+        L.or_fixmate.restype = C.c_int64
+        L.or_fixmate.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint64, C.c_uint64,
+                                 C.POINTER(C.c_int32)]
         _LIB = L
     return _LIB
 
@@ -281,3 +290,57 @@ def _regather(payload, offsets, order):
     for j, i in enumerate(order):
         out[new_off[j]:new_off[j + 1]] = payload[offsets[i]:offsets[i + 1]]
     return new_off, out
+
+
+# ---- read-name / CIGAR keyed consumers ---------------------------------
+def _pay(payload, offsets):
+    pay = np.ascontiguousarray(payload, np.uint8)
+    if pay.size == 0:
+        pay = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(offsets, np.uint64)
+    return pay, off, len(off) - 1
+
+
+def summarize_ranges(payload, offsets, split_status=0):
+    """SummarizeRecordReader (Summarize.java:664-755) over packed record payloads -> dict(key,
+    beg, end, rev, record, status)."""
+    pay, off, n = _pay(payload, offsets)
+    cap = 1
+    for i in range(n):  # upper bound: one range per CIGAR op + 1
+        cap += int(pay[int(off[i]) + 16]) | int(pay[int(off[i]) + 17]) << 8
+    cap += n
+    key = np.zeros(cap, np.int64)
+    beg = np.zeros(cap, np.int32)
+    end = np.zeros(cap, np.int32)
+    rev = np.zeros(cap, np.uint8)
+    rec = np.zeros(cap, np.uint32)
+    st = C.c_int32(0)
+    k = lib().or_summarize_ranges(pay.ctypes.data, off.ctypes.data, n, split_status, key.ctypes.data,
+                                  beg.ctypes.data, end.ctypes.data, rev.ctypes.data, rec.ctypes.data,
+                                  cap, C.byref(st))
+    assert k >= 0, k
+    return dict(key=key[:k], beg=beg[:k], end=end[:k], rev=rev[:k], record=rec[:k], status=st.value)
+
+
+def name_order(payload, offsets):
+    """FixMateMapper's shuffle order: (Text(readName), input order)."""
+    pay, off, n = _pay(payload, offsets)
+    perm = np.zeros(max(n, 1), np.uint32)
+    lib().or_name_order(pay.ctypes.data, off.ctypes.data, n, perm.ctypes.data)
+    return perm[:n]
+
+
+def fixmate(payload, offsets):
+    """FixMateReducer (FixMate.java:230-277) over the name-sorted records -> dict(payload,
+    offsets, src, status)."""
+    pay, off, n = _pay(payload, offsets)
+    cap = 2 * n + 1
+    pay_cap = 2 * int(off[-1]) + 16 * cap
+    out = np.zeros(max(pay_cap, 1), np.uint8)
+    ooff = np.zeros(cap + 1, np.uint64)
+    src = np.zeros(cap, np.uint32)
+    st = C.c_int32(0)
+    k = lib().or_fixmate(pay.ctypes.data, off.ctypes.data, n, out.ctypes.data, ooff.ctypes.data,
+                         src.ctypes.data, cap, pay_cap, C.byref(st))
+    assert k >= 0, k
+    return dict(payload=out[:int(ooff[k])], offsets=ooff[:k + 1], src=src[:k], status=st.value)

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Evidence pass on the current tree: GPU suite, smoke, bench line, rocprof kernel stats of the
+# same bench command.  Usage: tools/gpu_evidence.sh <outdir under gpurun_out/>
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-ev}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.txt 2>&1 &&
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 &&
+timeout -k 10 500 python -u bench.py --steps 5 --warmup 2 > $O/bench.json 2> $O/bench.err &&
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $O/rp -o bench --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --parity-splits 0 > $O/bench_rp.json 2> $O/bench_rp.err
