@@ -234,14 +234,21 @@ __global__ void k_edge_merge(const BlockRec* __restrict__ blk, const uint64_t* _
 }
 
 // LZ77 resolution of one block (phase 2 of the batched inflate); see resolve_dev.h.
-__global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk,
+#ifndef HBAM_RS_WAVES
+// waves per SIMD asked of the register allocator: 8 = the hardware maximum, which the 4.9 KiB of
+// LDS per block also allows (VGPRs 75 -> 64, 2 spilled): k_resolve 47.4 -> 42.6 ms at 10 GB
+#define HBAM_RS_WAVES 8
+#endif
+__global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* __restrict__ blk,
                                                 const uint64_t* __restrict__ uoff, uint32_t nblk,
                                                 uint8_t* __restrict__ ubuf,
                                                 const uint32_t* __restrict__ bitmap,
                                                 const uint32_t* __restrict__ tails,
                                                 int32_t* __restrict__ status) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[RS_BUF];
-  __shared__ uint64_t s_rec[RS_MAXM];   // pre matches from the front, ordered from the back
+  // match records, packed: index into s_pos (9 bits) | len-3 << 9 | dist-1 << 17 (u32 instead of
+  // the unpacked u64: 1.4 KiB less LDS per wave); pre matches from the front, ordered from the back
+  __shared__ uint32_t s_rec[RS_MAXM];
   __shared__ uint16_t s_pos[RS_MAXM];
   __shared__ uint64_t s_sel[8];
 #ifndef HBAM_RS_PREFIX
@@ -334,6 +341,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     for (uint32_t j0 = 0; j0 < total; j0 += 64) {
       const uint32_t j = j0 + lane;
       uint64_t rec = 0;
+      uint32_t pk = 0;
       bool pre = false, ord = false;
       if (j < total) {
         const uint32_t p = s_pos[j];
@@ -342,15 +350,16 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
         const uint32_t dist = ((dsc >> 8) & 0xffffu) + 1u;
         const uint32_t e = p - dist + (len < dist ? len : dist);
         rec = (uint64_t)p | (uint64_t)len << 16 | (uint64_t)dist << 32 | (uint64_t)e << 48;
+        pk = j | (len - 3u) << 9 | (dist - 1u) << 17;
         pre = e <= s0;
         ord = !pre;
         // a descriptor the Huffman pass cannot have written (source before the block, or a
         // hole past the block end): the block's tokens are corrupt
-        bad_desc |= dist > p || p + len > isize;
+        bad_desc |= dist > p || p + len > isize || dist > 32768u;
       }
       const uint64_t mp = __ballot(pre), mo = __ballot(ord);
-      if (pre) s_rec[npre + lane_rank(mp)] = rec;
-      if (ord) s_rec[RS_MAXM - 1 - (nord + lane_rank(mo))] = rec;
+      if (pre) s_rec[npre + lane_rank(mp)] = pk;
+      if (ord) s_rec[RS_MAXM - 1 - (nord + lane_rank(mo))] = pk;
       npre += (uint32_t)__popcll(mp);
       nord += (uint32_t)__popcll(mo);
     }
@@ -373,7 +382,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
 #endif
     const uint32_t lds_from = s0 - RS_W - a0;  // block offset of LDS index 0 (when s0 >= RS_W)
     for (uint32_t j = lane; j < npre; j += 64) {
-      const uint64_t rec = s_rec[j];
+      const uint64_t rec = rs_unpack(s_rec[j], s_pos);
       const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
                      dist = (uint32_t)(rec >> 32) & 0xffffu;
       const uint32_t src = p - dist;
@@ -402,11 +411,11 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
       // slots would cost the kernel half its occupancy)
       const uint32_t mine = nord > lane ? (nord - lane + 63u) / 64u : 0u;
       uint32_t live = mine >= 32u ? ~0u : (1u << mine) - 1u;
-      const uint64_t rec0 = mine ? s_rec[RS_MAXM - 1 - lane] : 0ull;
+      const uint64_t rec0 = mine ? rs_unpack(s_rec[RS_MAXM - 1 - lane], s_pos) : 0ull;
       if (mine) rs_bits(s_pend, ((uint32_t)rec0 & 0xffffu) - s0, (uint32_t)(rec0 >> 16) & 0xffffu, true);
 #pragma unroll 1
       for (uint32_t t = 1; t < mine; ++t) {
-        const uint64_t rec = s_rec[RS_MAXM - 1 - (lane + 64u * t)];
+        const uint64_t rec = rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos);
         rs_bits(s_pend, ((uint32_t)rec & 0xffffu) - s0, (uint32_t)(rec >> 16) & 0xffffu, true);
       }
       rs_lds_order();
@@ -427,12 +436,12 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
         uint32_t ready = (live & 1u) && is_ready(rec0) ? 1u : 0u;
 #pragma unroll 1
         for (uint32_t t = 1; t < mine; ++t)
-          if ((live >> t & 1u) && is_ready(s_rec[RS_MAXM - 1 - (lane + 64u * t)])) ready |= 1u << t;
+          if ((live >> t & 1u) && is_ready(rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos))) ready |= 1u << t;
         rs_lds_order();
         if (ready & 1u) run(rec0);
 #pragma unroll 1
         for (uint32_t t = 1; t < mine; ++t)
-          if (ready >> t & 1u) run(s_rec[RS_MAXM - 1 - (lane + 64u * t)]);
+          if (ready >> t & 1u) run(rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos));
         live &= ~ready;
 #ifdef HBAM_PROF
         ++n_bat;
@@ -449,7 +458,7 @@ __global__ __launch_bounds__(64) void k_resolve(const BlockRec* __restrict__ blk
     // ---- ordered matches: in-order batches
     for (uint32_t kk = 0; kk < nord;) {
       const uint32_t j = kk + lane;
-      const uint64_t rec = j < nord ? s_rec[RS_MAXM - 1 - j] : ~0ULL;
+      const uint64_t rec = j < nord ? rs_unpack(s_rec[RS_MAXM - 1 - j], s_pos) : ~0ULL;
       const uint32_t pk = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rec & 0xffffu);
       const bool ready = (j < nord) && (uint32_t)(rec >> 48) <= pk;
       const uint64_t nr = __ballot(!ready);

@@ -24,7 +24,10 @@
 namespace hbam {
 
 #ifndef HBAM_RS_W
-#define HBAM_RS_W 1024  // A/B at 2 GB (stretch 2 KiB): 4096 -> 20.0 ms, 2048 -> 18.0, 1024 -> 16.7; 0 is not supported
+// A/B at 2 GB (stretch 2 KiB): 4096 -> 20.0 ms, 2048 -> 18.0, 1024 -> 16.7; at 10 GB with packed
+// match records and 8 waves/SIMD (HBAM_RS_WAVES): 1024 -> 48.8 ms (LDS caps it at 7 waves), 512 ->
+// 42.6 ms (profiles/r02/s2/ab_resolve_occupancy_10g.txt); 0 is not supported
+#define HBAM_RS_W 512
 #endif
 #ifndef HBAM_RS_S
 #define HBAM_RS_S 1024  // A/B at 2 GB (window 1 KiB): 2048 -> 16.8 ms, 1024 -> 11.7 ms
@@ -39,6 +42,16 @@ constexpr uint32_t RS_MAXM = RS_S / 3 + 2;            // matches starting in one
 constexpr uint32_t RS_PW = (RS_S + 16 + 258 + 31) / 32 + 1;  // pending-byte words of a stretch + spill
 
 constexpr uint32_t RS_SLOTS = (RS_MAXM + 63) / 64;      // ordered matches per lane, at most
+static_assert(RS_MAXM <= 512, "packed match records hold a 9-bit s_pos index");
+
+// packed match record (s_pos index | len-3 << 9 | dist-1 << 17) -> p | len << 16 | dist << 32 |
+// e << 48, e = the end of the match's external source (p - dist + min(len, dist))
+__device__ __forceinline__ uint64_t rs_unpack(uint32_t pk, const uint16_t* s_pos) {
+  const uint32_t p = s_pos[pk & 511u];
+  const uint32_t len = ((pk >> 9) & 255u) + 3u, dist = (pk >> 17) + 1u;
+  const uint32_t e = p - dist + (len < dist ? len : dist);
+  return (uint64_t)p | (uint64_t)len << 16 | (uint64_t)dist << 32 | (uint64_t)e << 48;
+}
 
 // One wave per workgroup: LDS operations of a wave execute in issue order, so ordering the
 // lanes' LDS accesses needs no s_barrier, only that the compiler keep program order across

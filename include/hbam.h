@@ -349,8 +349,8 @@ int hbam_fixmate(hbam_ctx* ctx, const uint8_t* ubuf, const uint64_t* rec_off, ui
  * (len-3, dist-1 little-endian) at the start of every match hole, `bitmap` (host,
  * ceil(isize/32) words) one bit per match start, tail_token/tail_dist the final match shorter
  * than 3 bytes (op | n<<16 | 1<<31, or 0).  On return `io` holds the resolved bytes and
- * *status is HBAM_OK, or HBAM_EDATA when a token points outside the block (the pass refuses
- * such a block instead of copying from outside it). */
+ * *status is HBAM_OK, or HBAM_EDATA when a token points outside the block or has a distance
+ * above DEFLATE's 32768 (the pass refuses such a block instead of copying from outside it). */
 int hbam_resolve_tokens(hbam_ctx* ctx, uint8_t* io, uint32_t isize, const uint32_t* bitmap,
                         uint32_t tail_token, uint32_t tail_dist, int32_t* status);
 

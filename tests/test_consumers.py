@@ -350,11 +350,20 @@ def test_summarize_record_reader_mirror():
         want = o.summarize_ranges(pay, off, ref["status"])
         rr = consumers.SummarizeInputFormat().createRecordReader(sp, conf)
         keys, rngs = [], []
-        while rr.nextKeyValue():
-            keys.append(rr.getCurrentKey().get())
-            v = rr.getCurrentValue()
-            rngs.append((v.beg, v.end, int(v.reverseStrand)))
+        raised = 0
+        try:
+            while rr.nextKeyValue():
+                keys.append(rr.getCurrentKey().get())
+                v = rr.getCurrentValue()
+                rngs.append((v.beg, v.end, int(v.reverseStrand)))
+        except consumers.IndexOutOfBoundsException:
+            raised = -13
+        except formats.IllegalArgumentException:
+            raised = -6
+        except formats.SAMFormatException:
+            raised = -3
         rr.close()
+        assert raised == want["status"]
         assert keys == want["key"].tolist()
         assert rngs == list(zip(want["beg"].tolist(), want["end"].tolist(), want["rev"].tolist()))
 
