@@ -15,7 +15,7 @@ import htsjdk.samtools.util.RuntimeIOException;
 
 public final class Hbam implements AutoCloseable {
   public static final int OK = 0, EIO = -1, ETRUNC = -2, EFORMAT = -3, ERUNTIMEIO = -4,
-      EEOF = -5, EREFID = -6, EDATA = -7, EMORE = -12;
+      EEOF = -5, EREFID = -6, EDATA = -7, EMORE = -12, EINDEX = -13;
 
   private static final Linker LINKER = Linker.nativeLinker();
   private static final SymbolLookup LIB = SymbolLookup.libraryLookup(
@@ -45,6 +45,21 @@ public final class Hbam implements AutoCloseable {
       FunctionDescriptor.of(J, A, A, I, J, J, J, I, A));
   static final MethodHandle SPLITS = fn("hbam_probabilistic_splits",
       FunctionDescriptor.of(J, A, A, I, J, A, A, J, A, A));
+  // SURVEY.md §8 f-4: Summarize ranges, FixMate shuffle + reducer, device -> host copies
+  static final MethodHandle SUMMARIZE = fn("hbam_summarize_ranges", FunctionDescriptor.of(I, A, A, A));
+  static final MethodHandle NAME_ORDER = fn("hbam_name_order", FunctionDescriptor.of(I, A, A, A, J, A));
+  static final MethodHandle FIXMATE = fn("hbam_fixmate", FunctionDescriptor.of(I, A, A, A, J, A));
+  static final MethodHandle DOWNLOAD = fn("hbam_download", FunctionDescriptor.of(I, A, A, J, A));
+
+  /** hbam_ranges: n, status, pad, then the key / beg / end / rev / record device arrays. */
+  public static final StructLayout RANGES = MemoryLayout.structLayout(
+      J.withName("n"), I.withName("status"), I.withName("pad"), A.withName("key"), A.withName("beg"),
+      A.withName("end"), A.withName("rev"), A.withName("record"));
+  /** hbam_fixmate_run: n, payload_bytes, n_groups, status, pad, src / mate / offsets / payload. */
+  public static final StructLayout FIXMATE_RUN = MemoryLayout.structLayout(
+      J.withName("n"), J.withName("payload_bytes"), J.withName("n_groups"), I.withName("status"),
+      I.withName("pad"), A.withName("src"), A.withName("mate"), A.withName("offsets"),
+      A.withName("payload"));
 
   /** hbam_columns (include/hbam.h): 24 bytes of counts/status, then 27 pointer-sized slots
    *  (26 pointers and ubuf_len), 240 bytes in all. */
@@ -86,6 +101,7 @@ public final class Hbam implements AutoCloseable {
       case EREFID: return new IllegalArgumentException(where);
       case EDATA: return new RuntimeException(new java.util.zip.DataFormatException(where));
       case EIO: return new RuntimeIOException(new IOException(where));
+      case EINDEX: return new IndexOutOfBoundsException(where);
       default: return new RuntimeIOException("hbam error " + code + " at " + where);
     }
   }
@@ -100,6 +116,20 @@ public final class Hbam implements AutoCloseable {
   }
 
   public MemorySegment context() { return ctx; }
+
+  /** hbam_download: `bytes` of library-owned device memory into a new host segment of `arena`. */
+  public MemorySegment download(MemorySegment dev, long bytes, Arena arena) {
+    final MemorySegment h = arena.allocate(Math.max(bytes, 1), 16);
+    try {
+      final int rc = (int) DOWNLOAD.invokeExact(ctx, dev, bytes, h);
+      if (rc != OK) throw exceptionFor(rc, "hbam_download: " + lastError());
+    } catch (RuntimeException e) {
+      throw e;
+    } catch (Throwable t) {
+      throw new RuntimeException(t);
+    }
+    return h;
+  }
 
   @Override public void close() {
     try { DESTROY.invokeExact(ctx); } catch (Throwable t) { throw new RuntimeException(t); }

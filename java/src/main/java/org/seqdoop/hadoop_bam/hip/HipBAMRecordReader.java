@@ -94,7 +94,7 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
   }
 
   /** The file's bytes as one segment: mmap for the local file system, else read off-heap. */
-  private static MemorySegment mapFile(FileSystem fs, Path file, long len, Arena arena)
+  public static MemorySegment mapFile(FileSystem fs, Path file, long len, Arena arena)
       throws IOException {
     if (fs instanceof LocalFileSystem || "file".equals(fs.getUri().getScheme())) {
       try (FileChannel ch = FileChannel.open(java.nio.file.Path.of(file.toUri()),
