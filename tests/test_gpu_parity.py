@@ -379,7 +379,8 @@ def test_resolve_tokens_expands_matches(gpu_ctx):
     assert out == bytes(want)
 
 
-@pytest.mark.parametrize("case", ["dist_before_block", "hole_past_end", "tail_before_block"])
+@pytest.mark.parametrize("case", ["dist_before_block", "hole_past_end", "tail_before_block",
+                                  "dist_over_32k"])
 def test_resolve_forged_descriptor_is_an_error_not_a_hang(gpu_ctx, case):
     """A descriptor the Huffman pass could not have written (source before the block start, or
     a hole running past the block end) makes k_resolve refuse the block (HBAM_EDATA) instead of
@@ -395,6 +396,10 @@ def test_resolve_forged_descriptor_is_an_error_not_a_hang(gpu_ctx, case):
         p = isize - 10
         io[p:p + 3] = bytes([200, 0, 0])      # len 203 from p: runs past isize
         bm[p >> 5] |= np.uint32(1 << (p & 31))
+    elif case == "dist_over_32k":  # inside the block, but farther than DEFLATE's 32768
+        isize = 40000
+        io, bm = _tokens(list(range(64)) * 560 + [(100, 33000)] + [0] * (isize - 35940), isize)
+        io = bytearray(io)
     else:
         tail = (5 | 2 << 16 | 0x80000000, 9)  # 2 bytes at op 5 from dist 9 > 5
     rc, st, _ = gpu_ctx.resolve_tokens(bytes(io), bm, *tail)
