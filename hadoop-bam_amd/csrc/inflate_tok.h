@@ -48,6 +48,12 @@ namespace hbam {
 #define HBAM_TOK_K 4  // symbol-loop iterations per input epoch (power of two)
 #endif
 constexpr uint32_t TOK_K = HBAM_TOK_K;
+#ifndef HBAM_TOK_LIT3
+#define HBAM_TOK_LIT3 0  // A/B: up to three literals per fast-path iteration
+#endif
+// stream bits one fast-path iteration may consume: 2 lit/len codes + length extra + distance
+// code + distance extra = 15+15+5+15+13 = 63 (<= 64); with a third lit/len code 78 (<= 80)
+constexpr uint32_t TOK_FAST_BITS = HBAM_TOK_LIT3 ? 80u : 64u;
 constexpr uint32_t TOK_LENS_LL = 32;    // lens scratch: lit/len code lengths at +32 ..
 constexpr uint32_t TOK_LENS_D = 320;    //               distance code lengths at +320 (<= 30)
 
@@ -467,7 +473,20 @@ __device__ __forceinline__ uint32_t tok_fast(EIn& in, const HuffP& hl, const Huf
     if (sym < 256u) {
       if (op == isize) return 2u;
       sink.literal(op++, sym);
+#if HBAM_TOK_LIT3
+      // third lit/len code after two literals (the iteration's bit budget: TOK_FAST_BITS)
+      ein_refill(in);
+      if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) return 3u;
+      sym = (uint32_t)syms_ll[idx] | hi;
+      ein_drop(in, L);
+      if (sym < 256u) {
+        if (op == isize) return 2u;
+        sink.literal(op++, sym);
+        return 0u;
+      }
+#else
       return 0u;
+#endif
     }
   }
   if (sym == 256u) return 1u;
@@ -705,8 +724,8 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
         // epoch clock: the first active lane's, so the branch is scalar and every active lane
         // merges / requests its quad at the same iteration
         if ((__builtin_amdgcn_readfirstlane(++it) & (TOK_K - 1u)) == 0u) ein_epoch(in);
-        if (!ein_short(in, 64)) {  // else stall until the next epoch merges more input
-          if (in.total - in.consumed >= 64u)
+        if (!ein_short(in, TOK_FAST_BITS)) {  // else stall until the next epoch merges more input
+          if (in.total - in.consumed >= TOK_FAST_BITS)
             ex = tok_fast(in, hl, hd, syms_ll, syms_d, sink, op, isize);
           else
             ex = tok_careful(in, hl, hd, syms_ll, syms_d, sink, op, isize);
