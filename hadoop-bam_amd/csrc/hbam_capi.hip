@@ -65,6 +65,7 @@ enum BufId {
   B_PARTIAL,
   B_EVENTS,
   B_BADLIST,
+  B_MARK,
   // columns
   B_C_STATUS,
   B_C_BS,
@@ -971,13 +972,25 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   k_block_walk<<<grid_for(wb, 64), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, r0, hard_end, entry, rel,
                                                        count, exitp);
   uint32_t* nbad_d = (uint32_t*)(small + 5);
+  uint8_t* mark;
+  if ((rc = ensure(c, B_MARK, wb + 1, &mark))) return rc;
   HIPCHK(c, hipMemsetAsync(nbad_d, 0, 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(mark, 0, 1, c->stream));  // block 0 (the split start) is never listed
   if (wb > 1)
     k_stitch_check<<<grid_for(wb - 1, 256), 256, 0, c->stream>>>(entry, exitp, (uint32_t)wb, nbad_d,
-                                                                 badlist, (uint32_t)wb);
+                                                                 badlist, (uint32_t)wb, mark);
   uint32_t nbad = 0;
   HIPCHK(c, hipMemcpyAsync(&nbad, nbad_d, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (nbad) {  // runs of mismatched blocks repaired in parallel, then whatever is left, in order
+    k_chain_fix_par<<<grid_for(nbad, 64), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, entry, rel,
+                                                               count, exitp, badlist, nbad, mark);
+    HIPCHK(c, hipMemsetAsync(nbad_d, 0, 4, c->stream));
+    k_stitch_check<<<grid_for(wb - 1, 256), 256, 0, c->stream>>>(entry, exitp, (uint32_t)wb, nbad_d,
+                                                                 badlist, (uint32_t)wb, nullptr);
+    HIPCHK(c, hipMemcpyAsync(&nbad, nbad_d, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   if (nbad) {
     // sort the mismatch list (atomic order is arbitrary)
     std::vector<uint32_t> bl(nbad);

@@ -682,15 +682,42 @@ __global__ void k_block_walk(const uint8_t* __restrict__ u, const uint64_t* __re
   walk_one(u, uoff, b, r, hard_end, rel, count, exitp);
 }
 
-// mismatch list: blocks whose entry != predecessor's exit
+// mismatch list: blocks whose entry != predecessor's exit (mark: 1 per listed block, optional)
 __global__ void k_stitch_check(const uint64_t* __restrict__ entry, const uint64_t* __restrict__ exitp,
                                uint32_t nblk, uint32_t* __restrict__ nbad,
-                               uint32_t* __restrict__ bad_list, uint32_t cap) {
+                               uint32_t* __restrict__ bad_list, uint32_t cap, uint8_t* __restrict__ mark) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x + 1;
   if (b >= nblk) return;
-  if (entry[b] != exitp[b - 1]) {
+  const bool bad = entry[b] != exitp[b - 1];
+  if (mark) mark[b] = bad ? 1 : 0;
+  if (bad) {
     const uint32_t i = atomicAdd(nbad, 1u);
     if (i < cap) bad_list[i] = b;
+  }
+}
+
+// Parallel repair: one lane per run of mismatched blocks.  A listed block whose predecessor is
+// not listed heads a run; its lane re-walks it from the predecessor's exit and carries on while
+// the next block is still inconsistent, stopping before the next run head (owned by another
+// lane), so no two lanes write one block.  A head whose predecessor another lane re-walked may
+// start from a stale exit: the stitch check after this pass catches that, and k_chain_fix
+// finishes in order.
+__global__ void k_chain_fix_par(const uint8_t* __restrict__ u, const uint64_t* __restrict__ uoff,
+                                uint32_t nblk, uint64_t hard_end, uint64_t* __restrict__ entry,
+                                uint16_t* __restrict__ rel, uint32_t* __restrict__ count,
+                                uint64_t* __restrict__ exitp, const uint32_t* __restrict__ bad_list,
+                                uint32_t nbad, const uint8_t* __restrict__ mark) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nbad) return;
+  uint32_t b = bad_list[i];
+  if (mark[b - 1]) return;  // not a run head
+  for (;;) {
+    const uint64_t e = exitp[b - 1];
+    entry[b] = e;
+    walk_one(u, uoff, b, e, hard_end, rel, count, exitp);
+    ++b;
+    if (b >= nblk || (mark[b] && !mark[b - 1])) break;  // the end, or the next run's head
+    if (entry[b] == exitp[b - 1]) break;                 // consistent again
   }
 }
 

@@ -38,7 +38,11 @@ enum : int32_t {
 #define HBAM_NT_LOAD 0
 #endif
 #ifndef HBAM_NT_STORE
-#define HBAM_NT_STORE 1  // measured: input FETCH 6.1 -> 2.1 GB (= C) per 2 GB decode
+// Off: non-temporal token stores cut the Huffman pass's input FETCH to C (6.1 -> 2.1 GB per
+// 2 GB decode), but their write acknowledgements are slow and every epoch's `s_waitcnt vmcnt(0)`
+// (vmcnt counts stores too on CDNA) waits for the last iteration's stores: 105 -> 70 ms at
+// 10 GB with plain stores (profiles/r02/s2/ab_store_epoch_10g.txt).
+#define HBAM_NT_STORE 0
 #endif
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_quad(const uint4* p) {
