@@ -234,6 +234,21 @@ __global__ void k_edge_merge(const BlockRec* __restrict__ blk, const uint64_t* _
 }
 
 // LZ77 resolution of one block (phase 2 of the batched inflate); see resolve_dev.h.
+#ifndef HBAM_RS_LATE_WB
+#define HBAM_RS_LATE_WB 1  // A/B knob: stretch write-back issued after the raw prefetch
+#endif
+// one 16-byte column of a resolved stretch -> ubuf (bytewise where it overlaps a neighbour block)
+__device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64_t a, uint64_t base,
+                                              uint64_t aend, const uint4 v) {
+  if (a >= base && a + 16 <= aend) {
+    *(uint4*)(ubuf + a) = v;
+  } else if (a + 16 > base && a < aend) {
+    for (uint32_t t = 0; t < 16; ++t) {
+      const uint32_t wv = t < 4 ? v.x : t < 8 ? v.y : t < 12 ? v.z : v.w;
+      if (a + t >= base && a + t < aend) ubuf[a + t] = (uint8_t)(wv >> (8 * (t & 3)));
+    }
+  }
+}
 #ifndef HBAM_RS_WAVES
 // waves per SIMD asked of the register allocator: 8 = the hardware maximum, which the 4.9 KiB of
 // LDS per block also allows (VGPRs 75 -> 64, 2 spilled): k_resolve 47.4 -> 42.6 ms at 10 GB
@@ -500,20 +515,17 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
     p_bat += q2 - q1;
 #endif
     // ---- write back stretch k (LDS [RS_W, RS_W + RS_S)), then slide the window by RS_S
-    // (each lane moves its own 16-byte columns, so no barrier is needed inside the move)
+    // (each lane moves its own 16-byte columns, so no barrier is needed inside the move).
+    // The stretch is read into registers first and stored to ubuf after the prefetched raw
+    // stretch has been placed and the next one requested: the wait for that prefetch
+    // (vmcnt, which counts stores too) then never waits for this stretch's write-back.
+    uint4 wbv[RS_C];
 #pragma unroll
-    for (uint32_t h = 0; h < RS_S / 1024; ++h) {
-      const uint4 v = *(const uint4*)(s_buf + RS_W + 1024u * h + 16u * lane);
-      const uint64_t a = abase + s0 + 1024u * h + 16u * lane;
-      if (a >= base && a + 16 <= aend) {
-        *(uint4*)(ubuf + a) = v;
-      } else if (a + 16 > base && a < aend) {
-        for (uint32_t t = 0; t < 16; ++t) {
-          const uint32_t wv = t < 4 ? v.x : t < 8 ? v.y : t < 12 ? v.z : v.w;
-          if (a + t >= base && a + t < aend) ubuf[a + t] = (uint8_t)(wv >> (8 * (t & 3)));
-        }
-      }
-    }
+    for (uint32_t h = 0; h < RS_C; ++h) wbv[h] = *(const uint4*)(s_buf + RS_W + 1024u * h + 16u * lane);
+#if !HBAM_RS_LATE_WB
+#pragma unroll
+    for (uint32_t h = 0; h < RS_C; ++h) rs_write_back(ubuf, abase + s0 + 1024u * h + 16u * lane, base, aend, wbv[h]);
+#endif
     // move [RS_S, RS_S + RS_W + RS_S) down to 0 in 16-byte columns; one wave, so every read of
     // a 1 KiB step lands before that step's writes (any RS_W that is a multiple of 16)
 #pragma unroll
@@ -522,6 +534,10 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
     *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = ra0;
     if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = ra1;
     load_raw(k + 3, ra0, ra1);
+#if HBAM_RS_LATE_WB
+#pragma unroll
+    for (uint32_t h = 0; h < RS_C; ++h) rs_write_back(ubuf, abase + s0 + 1024u * h + 16u * lane, base, aend, wbv[h]);
+#endif
     __syncthreads();
 #ifdef HBAM_PROF
     p_wb += PROF_CLK() - q2;
