@@ -48,6 +48,12 @@ namespace hbam {
 #define HBAM_TOK_K 4  // symbol-loop iterations per input epoch (power of two)
 #endif
 constexpr uint32_t TOK_K = HBAM_TOK_K;
+
+#ifndef HBAM_TOK_PRED
+// fast path as one predicated path (tok_fast_pred) instead of the branching tok_fast: with plain
+// token stores 69.9 -> 67.9 ms at 10 GB (profiles/r02/s2/ab_pred_plainstores_10g.txt)
+#define HBAM_TOK_PRED 1
+#endif
 #ifndef HBAM_TOK_LIT3
 #define HBAM_TOK_LIT3 0  // A/B: up to three literals per fast-path iteration
 #endif
@@ -112,7 +118,7 @@ __device__ __forceinline__ void ein_refill(EIn& e) {
   }
 }
 // epoch boundary: merge the quad in flight into the free bank, request the next one
-__device__ __forceinline__ void ein_epoch(EIn& e) {
+__device__ __forceinline__ void ein_epoch_merge(EIn& e) {
   if (e.fp < e.fend && e.nv <= 4u) {
     const bool hi = (((e.rd + e.nv) & 7u) >> 2) != 0u;
     const u32x4_t t = e.t;
@@ -127,7 +133,11 @@ __device__ __forceinline__ void ein_epoch(EIn& e) {
     e.nv += 4u;
     ++e.fp;
   }
-  e.t = ein_load(e.fp < e.fend ? e.fp : e.safe);
+}
+__device__ __forceinline__ void ein_epoch_load(EIn& e) { e.t = ein_load(e.fp < e.fend ? e.fp : e.safe); }
+__device__ __forceinline__ void ein_epoch(EIn& e) {
+  ein_epoch_merge(e);
+  ein_epoch_load(e);
 }
 // bits the lane can use without another epoch
 __device__ __forceinline__ bool ein_short(const EIn& e, uint32_t need) {
@@ -346,6 +356,46 @@ struct TSink {
     }
     mark(op);
   }
+#if HBAM_TOK_PRED
+  // Predicated forms (A/B): the call is made by every lane of the iteration and `en` says
+  // whether it writes; only the chunk flush (a store) sits behind a branch.
+  __device__ __forceinline__ void switch_if(bool sw, uint32_t c) {
+    if (sw) flush();
+    curc = sw ? c : curc;
+    lo = sw ? 0ull : lo;
+    hi = sw ? 0ull : hi;
+  }
+  __device__ __forceinline__ void literal_if(bool en, uint32_t op, uint32_t b) {
+    const uint32_t r = soff + op, c = r >> 4;
+    switch_if(en && c != curc, c);
+    const uint64_t v = en ? (uint64_t)(b & 0xffu) << ((r & 7u) << 3) : 0ull;
+    const bool h = (r & 8u) != 0u;
+    hi |= h ? v : 0ull;
+    lo |= h ? 0ull : v;
+  }
+  __device__ __forceinline__ void match_if(bool en, uint32_t op, uint32_t n, uint32_t dist) {
+    if (en && n < 3u) {
+      tail[0] = op | n << 16 | 0x80000000u;
+      tail[1] = dist;
+    }
+    const bool em = en && n >= 3u;
+    const uint64_t d = em ? (uint64_t)((n - 3u) | (dist - 1u) << 8) : 0ull;
+    const uint32_t r = soff + op;
+    const uint32_t c = r >> 4, k = r & 15u;
+    switch_if(em && c != curc, c);
+    const uint32_t kl = k < 8u ? k : 0u, kh = k < 8u ? 0u : k - 8u;
+    lo |= k < 8u ? d << (8u * kl) : 0ull;
+    hi |= (k < 8u && k > 5u) ? d >> (64u - 8u * (k > 5u ? kl : 6u)) : 0ull;
+    hi |= k < 8u ? 0ull : d << (8u * kh);
+    const bool sp = em && k >= 14u;
+    if (sp) flush();
+    const uint64_t spill = d >> (8u * (16u - (k >= 14u ? k : 14u)));
+    curc = sp ? c + 1u : curc;
+    lo = sp ? spill : lo;
+    hi = sp ? 0ull : hi;
+    if (em) mark(op);
+  }
+#endif
   __device__ __forceinline__ void finish() {
     flush();
     while (bwin < nwin) {
@@ -513,6 +563,68 @@ __device__ __forceinline__ uint32_t tok_fast(EIn& in, const HuffP& hl, const Huf
   op += n;
   return n < mlen ? 2u : 0u;
 }
+#if HBAM_TOK_PRED
+// tok_fast as one predicated path (A/B): same outcomes and precedence; the first exit code a
+// lane meets wins, as the original's early returns.
+__device__ __forceinline__ uint32_t tok_fast_pred(EIn& in, const HuffP& hl, const HuffP& hd,
+                                                  const uint8_t* __restrict__ syms_ll,
+                                                  const uint8_t* __restrict__ syms_d, TSink& sink,
+                                                  uint32_t& op, uint32_t isize) {
+  ein_refill(in);
+  uint32_t ex = 0;
+  uint32_t L, idx, hi = 0;
+  const bool ok1 = huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi);
+  const uint32_t sym1 = ((uint32_t)syms_ll[ok1 ? idx : 0u] | hi);
+  ex = ok1 ? 0u : 3u;
+  ein_drop(in, ok1 ? L : 0u);
+  const bool lit1 = ok1 && sym1 < 256u;
+  ex = (ex == 0u && lit1 && op == isize) ? 2u : ex;
+  const bool emit1 = ex == 0u && lit1;
+  sink.literal_if(emit1, op, sym1);
+  op += emit1 ? 1u : 0u;
+  const bool ok2 = huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi);
+  const uint32_t sym2 = ((uint32_t)syms_ll[ok2 ? idx : 0u] | hi);
+  ex = (emit1 && !ok2) ? 3u : ex;
+  ein_drop(in, (emit1 && ok2) ? L : 0u);
+  const bool lit2 = emit1 && ok2 && sym2 < 256u;
+  ex = (ex == 0u && lit2 && op == isize) ? 2u : ex;
+  const bool emit2 = ex == 0u && lit2;
+  sink.literal_if(emit2, op, sym2);
+  op += emit2 ? 1u : 0u;
+  const uint32_t m = emit1 ? sym2 : sym1;
+  const bool ism = ex == 0u && !emit2 && !lit2;
+  ex = (ism && m == 256u) ? 1u : ex;
+  ex = (ism && m > 285u) ? 3u : ex;
+  const bool dom = ism && m > 256u && m <= 285u;
+  uint32_t lbase, lext;
+  length_base(dom ? m : 257u, lbase, lext);
+  ein_refill(in);
+  lext = dom ? lext : 0u;
+  const uint32_t mlen = lbase + ein_peek(in, lext);
+  ein_drop(in, lext);
+  uint32_t dh;
+  const bool okd = huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh);
+  const uint32_t dsym = syms_d[okd ? idx : 0u];
+  ex = (dom && !okd) ? 3u : ex;
+  ein_drop(in, (dom && okd) ? L : 0u);
+  ex = (dom && okd && dsym > 29u) ? 3u : ex;
+  const bool dom2 = dom && ex == 0u;
+  uint32_t dbase, dext;
+  dist_base(dom2 ? dsym : 0u, dbase, dext);
+  dext = dom2 ? dext : 0u;
+  const uint32_t dist = dbase + ein_peek(in, dext);
+  ein_drop(in, dext);
+  ex = (dom2 && op == isize) ? 2u : ex;
+  ex = (dom2 && ex == 0u && dist > op) ? 3u : ex;
+  const bool domatch = dom2 && ex == 0u;
+  uint32_t n = isize - op;
+  n = mlen < n ? mlen : n;
+  sink.match_if(domatch, op, n, dist);
+  op += domatch ? n : 0u;
+  ex = (domatch && n < mlen) ? 2u : ex;
+  return ex;
+}
+#endif
 // One symbol with every zlib outcome checked (the stream's last 64 bits).
 __device__ __forceinline__ uint32_t tok_careful(EIn& in, const HuffP& hl, const HuffP& hd,
                                                 const uint8_t* __restrict__ syms_ll,
@@ -726,7 +838,11 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
         if ((__builtin_amdgcn_readfirstlane(++it) & (TOK_K - 1u)) == 0u) ein_epoch(in);
         if (!ein_short(in, TOK_FAST_BITS)) {  // else stall until the next epoch merges more input
           if (in.total - in.consumed >= TOK_FAST_BITS)
+#if HBAM_TOK_PRED
+            ex = tok_fast_pred(in, hl, hd, syms_ll, syms_d, sink, op, isize);
+#else
             ex = tok_fast(in, hl, hd, syms_ll, syms_d, sink, op, isize);
+#endif
           else
             ex = tok_careful(in, hl, hd, syms_ll, syms_d, sink, op, isize);
         }

@@ -69,6 +69,15 @@ def main():
         print("  symbols/block %.0f, cycles/symbol %.1f, stalls/symbol %.3f, slow/symbol %.4f"
               % (sym / nb, tot / max(sym, 1), stall / max(sym, 1), slow / max(sym, 1)))
         print("  block cycles:", pct(R.sum(1)))
+        # LZ77 pass (k_resolve): slots 2 total, 3 setup, 4 descriptors, 5 ordered rounds,
+        # 12 pre matches, 13 write-back + slide; 6 rounds, 7 matches
+        Q = P[:, [2, 3, 4, 12, 5, 13]]
+        print("LZ77 pass, cycles per block (wave):")
+        for i, nm in enumerate(["total", "setup", "descriptors", "pre matches", "ordered rounds",
+                                "write-back+slide"]):
+            print("  %-16s %s" % (nm, pct(Q[:, i])))
+        print("  rounds/block %.0f, matches/block %.0f, cycles/round %.0f"
+              % (P[:, 6].mean(), P[:, 7].mean(), P[:, 5].sum() / max(P[:, 6].sum(), 1)))
     else:
         L.hbam_prof_attach_guess.argtypes = [C.c_void_p]
         k = a.guesses
