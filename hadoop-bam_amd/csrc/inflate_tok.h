@@ -54,8 +54,16 @@ constexpr uint32_t TOK_K = HBAM_TOK_K;
 #endif
 #ifndef HBAM_TOK_PRED
 // fast path as one predicated path (tok_fast_pred) instead of the branching tok_fast: with plain
-// token stores 69.9 -> 67.9 ms at 10 GB (profiles/r02/s2/ab_pred_plainstores_10g.txt)
+// token stores 69.9 -> 67.9 ms at 10 GB (profiles/r02/s2/ab_pred_plainstores_10g.txt).  The
+// cycle-stamp profiling build keeps the branching path: with the stamps in the loop, the
+// predicated one reported DataFormatException on 11k of 78k blocks of a 2 GB file that the
+// shipped build inflates CRC-clean (tools/check_inflate_crc.py: 8 files, 283k blocks, 0
+// mismatches), so the profile of that build would not describe the shipped kernel anyway.
+#ifdef HBAM_PROF
+#define HBAM_TOK_PRED 0
+#else
 #define HBAM_TOK_PRED 1
+#endif
 #endif
 #ifndef HBAM_TOK_LIT3
 #define HBAM_TOK_LIT3 0  // A/B: up to three literals per fast-path iteration
@@ -409,9 +417,12 @@ struct TSink {
     const uint32_t r = soff + op;
     const uint32_t c = r >> 4, k = r & 15u;
     switch_if(em && c != curc, c);
+    // every shift amount stays below 64 whichever arm the select keeps (a shift by 64 is
+    // undefined even when its result is discarded, and the optimizer may exploit it)
     const uint32_t kl = k < 8u ? k : 0u, kh = k < 8u ? 0u : k - 8u;
+    const uint32_t kr = (k > 5u && k < 8u) ? 64u - 8u * k : 8u;
     lo |= k < 8u ? d << (8u * kl) : 0ull;
-    hi |= (k < 8u && k > 5u) ? d >> (64u - 8u * (k > 5u ? kl : 6u)) : 0ull;
+    hi |= (k < 8u && k > 5u) ? d >> kr : 0ull;
     hi |= k < 8u ? 0ull : d << (8u * kh);
     const bool sp = em && k >= 14u;
     if (sp) flush();

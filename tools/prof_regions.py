@@ -15,7 +15,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "hadoop-bam_amd"), os.path.join(ROOT, "tools")]
-os.environ["HBAM_LIB"] = os.path.join(ROOT, "hadoop-bam_amd", "libhbam_prof.so")
+os.environ["HBAM_LIB"] = os.path.join(ROOT, "hadoop-bam_amd", os.environ.get("PROF_LIB", "libhbam_prof.so"))
 os.environ["HBAM_INFLATE_SLICES"] = "1"  # per-block prof slots are indexed per launch
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -53,7 +53,7 @@ def main():
         for _ in range(2):
             pbuf.zero_()
             rc, cols = ctx.decode_split_device(d[:n], h["first_voffset"], (n << 16) | 0xffff, h["n_ref"])
-            assert rc == 0 and cols.status == 0
+            assert rc == 0 and cols.status == 0, (rc, cols.status if rc == 0 else None, ctx.last_error())
         t = ctx.timing()
         print({k: round(v, 3) if isinstance(v, float) else v for k, v in t.items()}, flush=True)
         nb = t["n_blocks"]
