@@ -64,6 +64,8 @@ enum BufId {
   B_SMALL,
   B_PARTIAL,
   B_EVENTS,
+  B_EVFLAG,
+  B_EVPOS,
   B_BADLIST,
   B_MARK,
   // columns
@@ -418,15 +420,15 @@ __global__ void k_first_bad_block(const int32_t* __restrict__ st, const uint32_t
   if (bad) atomicMin(first, (unsigned long long)i);
 }
 
-__global__ void k_collect_empty(const BlockRec* __restrict__ blk, const uint64_t* __restrict__ uoff,
-                                uint64_t n, uint64_t* __restrict__ ev, uint32_t* __restrict__ nev,
-                                uint32_t cap) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
-  if (i >= n) return;
-  if (blk[i].isize == 0) {
-    const uint32_t k = atomicAdd(nev, 1u);
-    if (k < cap) ev[k] = uoff[i];
-  }
+// empty BGZF blocks after the first (block order): flag[j] = 1 for an ISIZE-0 block
+__global__ void k_empty_flags(const BlockRec* __restrict__ blk, uint64_t n, uint32_t* __restrict__ flag) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) flag[j] = (j >= 1 && blk[j].isize == 0) ? 1u : 0u;
+}
+__global__ void k_empty_scatter(const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ flag,
+                                const uint64_t* __restrict__ pos, uint64_t n, uint64_t* __restrict__ ev) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n && flag[j]) ev[pos[j]] = uoff[j];
 }
 
 int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint64_t nb,
@@ -939,18 +941,23 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
     HIPCHK(c, copy_sync(c, &u0, uoff + sblk, 8, hipMemcpyDeviceToHost));
     r0 = u0 + uoff_s;
   }
-  // events: empty blocks after the seek block, at positions <= hard_end
+  // events: empty blocks after the seek block, at positions <= hard_end, in block order (so
+  // sorted by position: k_decode_fixed binary-searches them; any number of them)
   uint64_t* evd;
-  if ((rc = ensure(c, B_EVENTS, 1024, &evd))) return rc;
-  uint32_t* nev_d = (uint32_t*)(small + 4);
-  HIPCHK(c, hipMemsetAsync(nev_d, 0, 4, c->stream));
-  if (nb > sblk + 1)
-    k_collect_empty<<<grid_for(nb - sblk - 1, 256), 256, 0, c->stream>>>(blk + sblk, uoff + sblk,
-                                                                         nb - sblk, evd, nev_d, 1024);
-  uint32_t nev = 0;
-  HIPCHK(c, hipMemcpyAsync(&nev, nev_d, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (nev > 1024) return set_err(c, HBAM_EUNSUPPORTED, "more than 1024 empty BGZF blocks in a split");
+  uint32_t* evflag;
+  uint64_t* evpos;
+  const uint64_t nbs = nb - sblk;
+  if ((rc = ensure(c, B_EVFLAG, nbs + 1, &evflag)) || (rc = ensure(c, B_EVPOS, nbs + 1, &evpos))) return rc;
+  k_empty_flags<<<grid_for(nbs, 256), 256, 0, c->stream>>>(blk + sblk, nbs, evflag);
+  HIPCHK(c, hipGetLastError());
+  uint64_t nev64 = 0;
+  if ((rc = scan_exclusive(c, evflag, nbs, evpos, &nev64))) return rc;
+  if ((rc = ensure(c, B_EVENTS, nev64 + 1, &evd))) return rc;
+  if (nev64)
+    k_empty_scatter<<<grid_for(nbs, 256), 256, 0, c->stream>>>(uoff + sblk, evflag, evpos, nbs, evd);
+  HIPCHK(c, hipGetLastError());
+  if (nev64 > 0xffffffffull) return set_err(c, HBAM_EUNSUPPORTED, "more than 2^32-1 empty BGZF blocks");
+  const uint32_t nev = (uint32_t)nev64;
   // events beyond the hard end cannot be reached; keep them (empty_at checks <= hard_end)
 
   // ---- K5: record starts (blocks [sblk, nb))

@@ -828,11 +828,16 @@ static __device__ uint64_t murmur3_java(const uint8_t* __restrict__ key, int32_t
 // call that starts exactly where an empty BGZF block follows returns -1; empty blocks
 // strictly inside a read are transparent; the hard end H (end of data, or the first block
 // that fails to read) ends every read.  decode() issues one read per field.
+// ev: the empty blocks' positions in ascending order (binary search; duplicates allowed)
 static __device__ __forceinline__ bool empty_at(const uint64_t* __restrict__ ev, uint32_t nev,
                                                 uint64_t p) {
-  for (uint32_t i = 0; i < nev; ++i)
-    if (ev[i] == p) return true;
-  return false;
+  uint32_t lo = 0, hi = nev;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ev[mid] < p) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < nev && ev[lo] == p;
 }
 
 __global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,

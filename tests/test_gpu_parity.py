@@ -63,6 +63,30 @@ def test_terminator_known_answer_on_device(gpu_ctx, oracle_mod):
     assert_same_split(got, ref)
 
 
+def test_thousands_of_empty_blocks(gpu_ctx, oracle_mod, genbam):
+    """An empty BGZF block after every data block (1329 of them, past the former 1024-entry
+    event list): the whole-file read and every guessed split equal the oracle's (a read that
+    meets an exhausted block followed by an empty one sees end-of-stream, htsjdk 1.131)."""
+    m = np.asarray(genbam.generate(records=260000, seed=11, straddle=0, empty_every=1, odd_every=13))
+    blocks = oracle_mod.scan_blocks(m)
+    assert int(np.sum(blocks["isize"] == 0)) > 1024
+    h = oracle_mod.read_header(m)
+    ref = oracle_mod.read_split(m, h["first_voffset"], _whole(m))
+    got = gpu_ctx.decode_split(m, h["first_voffset"], _whole(m), n_ref=h["n_ref"])
+    assert got["rc"] == 0, got
+    assert_same_split(got, ref)
+    b, e = oracle_mod.file_splits(len(m), 1 << 20)
+    want = oracle_mod.probabilistic_splits(m, b, e)
+    n, vs, ve = gpu_ctx.probabilistic_splits(m, b, e)
+    assert not isinstance(want, int) and n == len(want[0])
+    assert np.array_equal(vs, want[0]) and np.array_equal(ve, want[1])
+    for a, z in zip(vs, ve):
+        ref = oracle_mod.read_split(m, int(a), int(z))
+        got = gpu_ctx.decode_split(m, int(a), int(z), n_ref=h["n_ref"])
+        assert got["rc"] == 0, got
+        assert_same_split(got, ref)
+
+
 def _bgzf_block(payload, level=6):
     """One BGZF block (BSIZE/CRC/ISIZE as htsjdk writes them) holding `payload`."""
     import struct
