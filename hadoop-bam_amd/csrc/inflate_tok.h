@@ -65,6 +65,12 @@ constexpr uint32_t TOK_K = HBAM_TOK_K;
 #define HBAM_TOK_PRED 1
 #endif
 #endif
+#ifndef HBAM_TOK_SPEC
+// fast path tok_fast_spec: decode first, then the iteration's output as one packet (TSink::put):
+// 66.4 -> 60.3 ms at 10 GB (profiles/r02/s2/ab_spec_10g.txt; the same decode order with the
+// three separate sink calls: 66.7 ms)
+#define HBAM_TOK_SPEC 1
+#endif
 #ifndef HBAM_TOK_LIT3
 #define HBAM_TOK_LIT3 0  // A/B: up to three literals per fast-path iteration
 #endif
@@ -432,6 +438,27 @@ struct TSink {
     hi = sp ? 0ull : hi;
     if (em) mark(op);
   }
+  // One iteration's output as one packet: nb (<= 5) bytes P (LSB first) at ubuf position
+  // soff + op: up to two literals and a 3-byte match descriptor, always contiguous, so one
+  // chunk switch and at most one spill into the next chunk (tok_fast_spec).
+  __device__ __forceinline__ void put(uint32_t op, uint64_t P, uint32_t nb) {
+    const bool any = nb != 0u;
+    const uint32_t r = soff + op;
+    const uint32_t c = r >> 4, k = r & 15u;
+    switch_if(any && c != curc, c);
+    // shift amounts below 64 in every select arm (P < 2^40)
+    const uint32_t kl = k < 8u ? k : 0u, kh = k < 8u ? 0u : k - 8u;
+    const uint32_t kr = (k > 3u && k < 8u) ? 64u - 8u * k : 8u;
+    lo |= k < 8u ? P << (8u * kl) : 0ull;
+    hi |= (k > 3u && k < 8u) ? P >> kr : 0ull;
+    hi |= k < 8u ? 0ull : P << (8u * kh);
+    const bool sp = any && k + nb > 16u;
+    if (sp) flush();
+    const uint64_t spill = P >> (8u * (16u - (k >= 12u ? k : 12u)));
+    curc = sp ? c + 1u : curc;
+    lo = sp ? spill : lo;
+    hi = sp ? 0ull : hi;
+  }
 #endif
   __device__ __forceinline__ void finish() {
     flush();
@@ -661,6 +688,82 @@ __device__ __forceinline__ uint32_t tok_fast_pred(EIn& in, const HuffP& hl, cons
   ex = (domatch && n < mlen) ? 2u : ex;
   return ex;
 }
+#if HBAM_TOK_SPEC
+// tok_fast_pred with the decode and the output separated: both lit/len lookups run before
+// either symbol read (the second on the bits after the first code, whether or not it turns
+// out to be used), so the two LDS reads are in flight together; the iteration's bytes (up to
+// two literals and a match descriptor, contiguous) then go to the sink as one packet: one
+// chunk-switch test and one spill test per iteration instead of one of each per token.
+// Same outcomes and precedence as tok_fast_pred.
+__device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, const HuffP& hd,
+                                                  const uint8_t* __restrict__ syms_ll,
+                                                  const uint8_t* __restrict__ syms_d, TSink& sink,
+                                                  uint32_t& op, uint32_t isize) {
+  ein_refill(in);
+  uint32_t L1, idx1, hi1 = 0, L2, idx2, hi2 = 0;
+  const bool ok1 = huffp_lookup<true>(hl, ein_rev15(in), L1, idx1, hi1);
+  const uint32_t l1 = ok1 ? L1 : 0u;
+  const uint32_t v2 = __builtin_bitreverse32((uint32_t)(in.bb >> l1)) >> 17;
+  const bool ok2 = huffp_lookup<true>(hl, v2, L2, idx2, hi2);
+  const uint32_t sym1 = (uint32_t)syms_ll[ok1 ? idx1 : 0u] | hi1;
+  const uint32_t sym2 = (uint32_t)syms_ll[ok2 ? idx2 : 0u] | hi2;
+  uint32_t ex = ok1 ? 0u : 3u;
+  ein_drop(in, l1);
+  const bool lit1 = ok1 && sym1 < 256u;
+  ex = (ex == 0u && lit1 && op == isize) ? 2u : ex;
+  const bool emit1 = ex == 0u && lit1;
+  const uint32_t op1 = op;
+  op += emit1 ? 1u : 0u;
+  ex = (emit1 && !ok2) ? 3u : ex;
+  ein_drop(in, (emit1 && ok2) ? L2 : 0u);
+  const bool lit2 = emit1 && ok2 && sym2 < 256u;
+  ex = (ex == 0u && lit2 && op == isize) ? 2u : ex;
+  const bool emit2 = ex == 0u && lit2;
+  op += emit2 ? 1u : 0u;
+  const uint32_t m = emit1 ? sym2 : sym1;
+  const bool ism = ex == 0u && !emit2 && !lit2;
+  ex = (ism && m == 256u) ? 1u : ex;
+  ex = (ism && m > 285u) ? 3u : ex;
+  const bool dom = ism && m > 256u && m <= 285u;
+  uint32_t lbase, lext;
+  length_base(dom ? m : 257u, lbase, lext);
+  ein_refill(in);
+  lext = dom ? lext : 0u;
+  const uint32_t mlen = lbase + ein_peek(in, lext);
+  ein_drop(in, lext);
+  uint32_t L, idx, dh;
+  const bool okd = huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh);
+  const uint32_t dsym = syms_d[okd ? idx : 0u];
+  ex = (dom && !okd) ? 3u : ex;
+  ein_drop(in, (dom && okd) ? L : 0u);
+  ex = (dom && okd && dsym > 29u) ? 3u : ex;
+  const bool dom2 = dom && ex == 0u;
+  uint32_t dbase, dext;
+  dist_base(dom2 ? dsym : 0u, dbase, dext);
+  dext = dom2 ? dext : 0u;
+  const uint32_t dist = dbase + ein_peek(in, dext);
+  ein_drop(in, dext);
+  ex = (dom2 && op == isize) ? 2u : ex;
+  ex = (dom2 && ex == 0u && dist > op) ? 3u : ex;
+  const bool domatch = dom2 && ex == 0u;
+  uint32_t n = isize - op;
+  n = mlen < n ? mlen : n;
+  if (domatch && n < 3u) {  // the output filled up inside the match: last token of the block
+    sink.tail[0] = op | n << 16 | 0x80000000u;
+    sink.tail[1] = dist;
+  }
+  const bool em = domatch && n >= 3u;
+  uint64_t P = emit1 ? (uint64_t)(sym1 & 0xffu) : 0ull;
+  P |= emit2 ? (uint64_t)(sym2 & 0xffu) << 8 : 0ull;
+  const uint32_t nl = (emit1 ? 1u : 0u) + (emit2 ? 1u : 0u);
+  P |= em ? (uint64_t)((n - 3u) | (dist - 1u) << 8) << (8u * nl) : 0ull;
+  sink.put(op1, P, nl + (em ? 3u : 0u));
+  if (em) sink.mark(op);
+  op += domatch ? n : 0u;
+  ex = (domatch && n < mlen) ? 2u : ex;
+  return ex;
+}
+#endif
 #endif
 // One symbol with every zlib outcome checked (the stream's last 64 bits).
 __device__ __forceinline__ uint32_t tok_careful(EIn& in, const HuffP& hl, const HuffP& hd,
@@ -875,7 +978,9 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
         if ((__builtin_amdgcn_readfirstlane(++it) & (TOK_K - 1u)) == 0u) ein_epoch(in);
         if (!ein_short(in, TOK_FAST_BITS)) {  // else stall until the next epoch merges more input
           if (in.total - in.consumed >= TOK_FAST_BITS)
-#if HBAM_TOK_PRED
+#if HBAM_TOK_PRED && HBAM_TOK_SPEC
+            ex = tok_fast_spec(in, hl, hd, syms_ll, syms_d, sink, op, isize);
+#elif HBAM_TOK_PRED
             ex = tok_fast_pred(in, hl, hd, syms_ll, syms_d, sink, op, isize);
 #else
             ex = tok_fast(in, hl, hd, syms_ll, syms_d, sink, op, isize);
