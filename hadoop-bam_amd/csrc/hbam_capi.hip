@@ -66,6 +66,8 @@ enum BufId {
   B_EVENTS,
   B_EVFLAG,
   B_EVPOS,
+  B_ORDER,
+  B_ORDHIST,
   B_BADLIST,
   B_MARK,
   // columns
@@ -431,6 +433,60 @@ __global__ void k_empty_scatter(const uint64_t* __restrict__ uoff, const uint32_
   if (j < n && flag[j]) ev[pos[j]] = uoff[j];
 }
 
+// Lane order of the Huffman pass (HBAM_TOK_ORDER): a wave of 64 lanes runs as long as its
+// slowest block, so blocks of similar size share a wave and the largest go first.  Counting
+// sort by compressed length in 256-byte classes, longest class first (order inside a class is
+// arbitrary: every output of the pass is indexed by block, not by lane).
+#ifndef HBAM_TOK_ORDER
+#define HBAM_TOK_ORDER 0
+#endif
+__device__ __forceinline__ uint32_t order_class(uint32_t clen) {
+  const uint32_t k = clen >> 8;
+  return 255u - (k < 255u ? k : 255u);
+}
+__global__ __launch_bounds__(256) void k_order_hist(const BlockRec* __restrict__ blk, uint32_t n,
+                                                    uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i < n) atomicAdd(&h[order_class(blk[i].clen)], 1u);
+  __syncthreads();
+  if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+__global__ __launch_bounds__(256) void k_order_scan(uint32_t* __restrict__ hist) {  // 1 x 256
+  __shared__ uint32_t s[256];
+  s[threadIdx.x] = hist[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < 256u; ++k) {
+      const uint32_t v = s[k];
+      s[k] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  hist[threadIdx.x] = s[threadIdx.x];
+}
+__global__ __launch_bounds__(256) void k_order_scatter(const BlockRec* __restrict__ blk, uint32_t n,
+                                                       uint32_t* __restrict__ cursor,
+                                                       uint32_t* __restrict__ order) {
+  __shared__ uint32_t h[256], base[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  uint32_t cls = 0, r = 0;
+  if (i < n) {
+    cls = order_class(blk[i].clen);
+    r = atomicAdd(&h[cls], 1u);
+  }
+  __syncthreads();
+  if (h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], h[threadIdx.x]);
+  __syncthreads();
+  if (i < n) order[base[cls] + r] = i;
+}
+
 int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint64_t nb,
                    const uint64_t* uoff, uint8_t* ubuf, int32_t* st, bool want_crc, uint32_t* crc) {
   uint8_t* lens;
@@ -441,6 +497,10 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   if ((rc = ensure(c, B_BITMAP, nb * BITMAP_WORDS, &bitmap))) return rc;
   if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
   if ((rc = ensure(c, B_EDGE, 32 * nb + 32, &edges))) return rc;
+  uint32_t *order = nullptr, *ohist = nullptr;
+  if (HBAM_TOK_ORDER && nb) {
+    if ((rc = ensure(c, B_ORDER, nb, &order)) || (rc = ensure(c, B_ORDHIST, 256, &ohist))) return rc;
+  }
   // Both passes are latency-bound at low occupancy (Huffman: 2 waves/SIMD; LZ77: a serial
   // walk per block), so the blocks are cut into slices and the LZ77 pass of slice s runs on a
   // second stream beside the Huffman pass of slice s+1: the CUs interleave the two kernels'
@@ -456,9 +516,15 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
       const uint64_t lo = nb * si / ns, hi = nb * (si + 1) / ns, n = hi - lo;
       if (!n) continue;
       hipStream_t rs = ns > 1 ? c->stream2 : c->stream;
+      if (order) {
+        HIPCHK(c, hipMemsetAsync(ohist, 0, 256 * sizeof(uint32_t), c->stream));
+        k_order_hist<<<grid_for(n, 256), 256, 0, c->stream>>>(blk + lo, (uint32_t)n, ohist);
+        k_order_scan<<<1, 256, 0, c->stream>>>(ohist);
+        k_order_scatter<<<grid_for(n, 256), 256, 0, c->stream>>>(blk + lo, (uint32_t)n, ohist, order + lo);
+      }
       k_inflate_tokens<<<grid_for(n, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
           dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf, lens + lo * LENS_SLOT, bitmap + lo * BITMAP_WORDS,
-          tails + 2 * lo, edges + 32 * lo, st + lo);
+          tails + 2 * lo, edges + 32 * lo, st + lo, order ? order + lo : nullptr);
       if (ns > 1) {
         HIPCHK(c, hipEventRecord(c->slice_ev[si], c->stream));
         HIPCHK(c, hipStreamWaitEvent(rs, c->slice_ev[si], 0));

@@ -19,6 +19,8 @@ ap.add_argument("--size", type=float, default=2e9)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--seed", type=int, default=2)
 ap.add_argument("--libs", nargs="+", default=["libhbam.so"])
+ap.add_argument("--orders", nargs="+", default=["file"],
+                help="block order handed to hbam_inflate: file, clen (descending), shuffle")
 ap.add_argument("--slices", nargs="+", type=int, default=[0], help="HBAM_INFLATE_SLICES values (0: library default)")
 a = ap.parse_args()
 g = genbam.generate(target_bytes=int(a.size), seed=a.seed, threads=16)
@@ -27,7 +29,7 @@ d = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
 d[:len(data)].copy_(torch.from_numpy(data))
 d[len(data):].zero_()
 torch.cuda.synchronize()
-for lib, sl in [(x, y) for x in a.libs for y in a.slices]:
+for lib, sl, order in [(x, y, z) for x in a.libs for y in a.slices for z in a.orders]:
     if sl:
         os.environ["HBAM_INFLATE_SLICES"] = str(sl)
     else:
@@ -38,6 +40,12 @@ for lib, sl in [(x, y) for x in a.libs for y in a.slices]:
     rc, blocks = ctx.scan_blocks(d[:len(data)])
     assert rc == 0, rc
     n = len(blocks["coff"])
+    perm = np.arange(n)
+    if order == "clen":
+        perm = np.argsort(-blocks["clen"].astype(np.int64), kind="stable")
+    elif order == "shuffle":
+        perm = np.random.default_rng(1).permutation(n)
+    blocks = {k: v[perm] for k, v in blocks.items()}
     arr = (_lib.Block * n)()
     for i in range(n):
         arr[i].coff = int(blocks["coff"][i]); arr[i].clen = int(blocks["clen"][i])
@@ -48,7 +56,7 @@ for lib, sl in [(x, y) for x in a.libs for y in a.slices]:
         rc = L.hbam_inflate(ctx.h, C.c_void_p(d.data_ptr()), 1, len(data), arr, n, 0, None, 0,
                             off.ctypes.data, st.ctypes.data)
         t = ctx.timing()
-        print("%-18s slices %d rep %d rc %d blocks %d U %.3f GB huffman %.3f ms resolve %.3f ms bad %d"
-              % (lib, sl, r, rc, n, off[-1] / 1e9, t["huffman_ms"], t["resolve_ms"], int(np.sum(st != 0))),
+        print("%-18s order %-7s slices %d rep %d rc %d blocks %d U %.3f GB huffman %.3f ms resolve %.3f ms bad %d"
+              % (lib, order, sl, r, rc, n, off[-1] / 1e9, t["huffman_ms"], t["resolve_ms"], int(np.sum(st != 0))),
               flush=True)
     ctx.close()
