@@ -71,6 +71,9 @@ constexpr uint32_t TOK_K = HBAM_TOK_K;
 // three separate sink calls: 66.7 ms)
 #define HBAM_TOK_SPEC 1
 #endif
+#ifndef HBAM_TOK_MARK1
+#define HBAM_TOK_MARK1 0  // A/B: match-start bitmap window change as an if + rare zero loop
+#endif
 #ifndef HBAM_TOK_LIT3
 #define HBAM_TOK_LIT3 0  // A/B: up to three literals per fast-path iteration
 #endif
@@ -353,11 +356,21 @@ struct TSink {
   }
   __device__ __forceinline__ void mark(uint32_t op) {
     const uint32_t w = op >> 7;
+#if HBAM_TOK_MARK1
+    // one window change per call in the common case; windows skipped by a long match or a
+    // literal run (no match start in them) are stored as zeros in a rarely taken loop
+    if (bwin < w) {
+      win_store();
+      w0 = w1 = w2 = w3 = 0;
+      for (++bwin; bwin < w; ++bwin) win_store();
+    }
+#else
     while (bwin < w) {
       win_store();
       w0 = w1 = w2 = w3 = 0;
       ++bwin;
     }
+#endif
     const uint32_t i = op & 127u, m = 1u << (i & 31u), q = i >> 5;
     w0 |= q == 0u ? m : 0u;
     w1 |= q == 1u ? m : 0u;
