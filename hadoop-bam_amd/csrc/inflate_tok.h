@@ -451,7 +451,7 @@ struct TSink {
     hi = sp ? 0ull : hi;
     if (em) mark(op);
   }
-  // One iteration's output as one packet: nb (<= 5) bytes P (LSB first) at ubuf position
+  // One iteration's output as one packet: nb (<= 5, or 6 with HBAM_TOK_LIT3) bytes P (LSB first) at ubuf position
   // soff + op: up to two literals and a 3-byte match descriptor, always contiguous, so one
   // chunk switch and at most one spill into the next chunk (tok_fast_spec).
   __device__ __forceinline__ void put(uint32_t op, uint64_t P, uint32_t nb) {
@@ -459,15 +459,15 @@ struct TSink {
     const uint32_t r = soff + op;
     const uint32_t c = r >> 4, k = r & 15u;
     switch_if(any && c != curc, c);
-    // shift amounts below 64 in every select arm (P < 2^40)
+    // shift amounts below 64 in every select arm (P < 2^48: at most 6 bytes)
     const uint32_t kl = k < 8u ? k : 0u, kh = k < 8u ? 0u : k - 8u;
-    const uint32_t kr = (k > 3u && k < 8u) ? 64u - 8u * k : 8u;
+    const uint32_t kr = (k > 1u && k < 8u) ? 64u - 8u * k : 8u;
     lo |= k < 8u ? P << (8u * kl) : 0ull;
-    hi |= (k > 3u && k < 8u) ? P >> kr : 0ull;
+    hi |= (k > 1u && k < 8u) ? P >> kr : 0ull;
     hi |= k < 8u ? 0ull : P << (8u * kh);
     const bool sp = any && k + nb > 16u;
     if (sp) flush();
-    const uint64_t spill = P >> (8u * (16u - (k >= 12u ? k : 12u)));
+    const uint64_t spill = P >> (8u * (16u - (k >= 10u ? k : 10u)));
     curc = sp ? c + 1u : curc;
     lo = sp ? spill : lo;
     hi = sp ? 0ull : hi;
@@ -733,8 +733,24 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   ex = (ex == 0u && lit2 && op == isize) ? 2u : ex;
   const bool emit2 = ex == 0u && lit2;
   op += emit2 ? 1u : 0u;
+#if HBAM_TOK_LIT3
+  // a third lit/len code after two literals (bit budget TOK_FAST_BITS = 80: one refill here)
+  ein_refill(in);
+  uint32_t L3, idx3, hi3 = 0;
+  const bool ok3 = huffp_lookup<true>(hl, ein_rev15(in), L3, idx3, hi3);
+  const uint32_t sym3 = (uint32_t)syms_ll[ok3 ? idx3 : 0u] | hi3;
+  ex = (emit2 && !ok3) ? 3u : ex;
+  ein_drop(in, (emit2 && ok3) ? L3 : 0u);
+  const bool lit3 = emit2 && ok3 && sym3 < 256u;
+  ex = (ex == 0u && lit3 && op == isize) ? 2u : ex;
+  const bool emit3 = ex == 0u && lit3;
+  op += emit3 ? 1u : 0u;
+  const uint32_t m = emit2 ? sym3 : emit1 ? sym2 : sym1;
+  const bool ism = ex == 0u && (emit2 ? !lit3 : emit1 ? !lit2 : !lit1);
+#else
   const uint32_t m = emit1 ? sym2 : sym1;
   const bool ism = ex == 0u && !emit2 && !lit2;
+#endif
   ex = (ism && m == 256u) ? 1u : ex;
   ex = (ism && m > 285u) ? 3u : ex;
   const bool dom = ism && m > 256u && m <= 285u;
@@ -768,7 +784,12 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   const bool em = domatch && n >= 3u;
   uint64_t P = emit1 ? (uint64_t)(sym1 & 0xffu) : 0ull;
   P |= emit2 ? (uint64_t)(sym2 & 0xffu) << 8 : 0ull;
+#if HBAM_TOK_LIT3
+  P |= emit3 ? (uint64_t)(sym3 & 0xffu) << 16 : 0ull;
+  const uint32_t nl = (emit1 ? 1u : 0u) + (emit2 ? 1u : 0u) + (emit3 ? 1u : 0u);
+#else
   const uint32_t nl = (emit1 ? 1u : 0u) + (emit2 ? 1u : 0u);
+#endif
   P |= em ? (uint64_t)((n - 3u) | (dist - 1u) << 8) << (8u * nl) : 0ull;
   sink.put(op1, P, nl + (em ? 3u : 0u));
   if (em) sink.mark(op);
