@@ -179,6 +179,39 @@ def parity_at_size(ctx, buf, dbuf, n_splits, seed, threads):
                     "column and every record byte vs the oracle"}
 
 
+def free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N rank processes (one per GPU) with
+    the torch.distributed env of a single-node job, before this process touches a GPU; wait for
+    all, end the others when one fails, and return the worst exit status."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(os.environ.get("MASTER_PORT") or free_port()))
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            r = p.poll()
+            if r is None:
+                continue
+            procs.remove(p)
+            if r != 0:
+                rc = rc or r
+                for q in procs:  # a rank died: the others would wait at a collective forever
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -191,17 +224,24 @@ def main():
     ap.add_argument("--parity-splits", type=int, default=32)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d (launch with N ranks, or without a "
+                         "launcher and let bench.py start them)" % (args.gpus, world))
     threads = host_threads()
     import torch
     dist = None
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     # RCCL between GPUs; HBAM_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks on
     # one GPU (host-staged collectives), which is how it is tested on the one-GPU pool
     backend = os.environ.get("HBAM_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     cdev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
         import torch.distributed as dist

@@ -66,8 +66,6 @@ enum BufId {
   B_EVENTS,
   B_EVFLAG,
   B_EVPOS,
-  B_ORDER,
-  B_ORDHIST,
   B_BADLIST,
   B_MARK,
   // columns
@@ -112,6 +110,7 @@ enum BufId {
   B_G_CUBUF,
   B_G_CST,
   B_G_CCRC,
+  B_G_WIN,  // caller-gathered guess windows staged from the host
   B_S_UK0,
   B_S_UK1,
   B_S_V0,
@@ -123,6 +122,8 @@ enum BufId {
   B_S_PERM,
   B_S_RECOFF,
   B_S_BOUNDS,
+  B_M_MAP,  // multi-input Sort: merged index per input index
+  B_M_ERR,
   B_DF_SRC,
   B_DF_TOK,
   B_DF_NTOK,
@@ -433,60 +434,6 @@ __global__ void k_empty_scatter(const uint64_t* __restrict__ uoff, const uint32_
   if (j < n && flag[j]) ev[pos[j]] = uoff[j];
 }
 
-// Lane order of the Huffman pass (HBAM_TOK_ORDER): a wave of 64 lanes runs as long as its
-// slowest block, so blocks of similar size share a wave and the largest go first.  Counting
-// sort by compressed length in 256-byte classes, longest class first (order inside a class is
-// arbitrary: every output of the pass is indexed by block, not by lane).
-#ifndef HBAM_TOK_ORDER
-#define HBAM_TOK_ORDER 0
-#endif
-__device__ __forceinline__ uint32_t order_class(uint32_t clen) {
-  const uint32_t k = clen >> 8;
-  return 255u - (k < 255u ? k : 255u);
-}
-__global__ __launch_bounds__(256) void k_order_hist(const BlockRec* __restrict__ blk, uint32_t n,
-                                                    uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i < n) atomicAdd(&h[order_class(blk[i].clen)], 1u);
-  __syncthreads();
-  if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
-}
-__global__ __launch_bounds__(256) void k_order_scan(uint32_t* __restrict__ hist) {  // 1 x 256
-  __shared__ uint32_t s[256];
-  s[threadIdx.x] = hist[threadIdx.x];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (uint32_t k = 0; k < 256u; ++k) {
-      const uint32_t v = s[k];
-      s[k] = acc;
-      acc += v;
-    }
-  }
-  __syncthreads();
-  hist[threadIdx.x] = s[threadIdx.x];
-}
-__global__ __launch_bounds__(256) void k_order_scatter(const BlockRec* __restrict__ blk, uint32_t n,
-                                                       uint32_t* __restrict__ cursor,
-                                                       uint32_t* __restrict__ order) {
-  __shared__ uint32_t h[256], base[256];
-  h[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  uint32_t cls = 0, r = 0;
-  if (i < n) {
-    cls = order_class(blk[i].clen);
-    r = atomicAdd(&h[cls], 1u);
-  }
-  __syncthreads();
-  if (h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], h[threadIdx.x]);
-  __syncthreads();
-  if (i < n) order[base[cls] + r] = i;
-}
-
 int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint64_t nb,
                    const uint64_t* uoff, uint8_t* ubuf, int32_t* st, bool want_crc, uint32_t* crc) {
   uint8_t* lens;
@@ -497,10 +444,6 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   if ((rc = ensure(c, B_BITMAP, nb * BITMAP_WORDS, &bitmap))) return rc;
   if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
   if ((rc = ensure(c, B_EDGE, 32 * nb + 32, &edges))) return rc;
-  uint32_t *order = nullptr, *ohist = nullptr;
-  if (HBAM_TOK_ORDER && nb) {
-    if ((rc = ensure(c, B_ORDER, nb, &order)) || (rc = ensure(c, B_ORDHIST, 256, &ohist))) return rc;
-  }
   // Both passes are latency-bound at low occupancy (Huffman: 2 waves/SIMD; LZ77: a serial
   // walk per block), so the blocks are cut into slices and the LZ77 pass of slice s runs on a
   // second stream beside the Huffman pass of slice s+1: the CUs interleave the two kernels'
@@ -516,15 +459,9 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
       const uint64_t lo = nb * si / ns, hi = nb * (si + 1) / ns, n = hi - lo;
       if (!n) continue;
       hipStream_t rs = ns > 1 ? c->stream2 : c->stream;
-      if (order) {
-        HIPCHK(c, hipMemsetAsync(ohist, 0, 256 * sizeof(uint32_t), c->stream));
-        k_order_hist<<<grid_for(n, 256), 256, 0, c->stream>>>(blk + lo, (uint32_t)n, ohist);
-        k_order_scan<<<1, 256, 0, c->stream>>>(ohist);
-        k_order_scatter<<<grid_for(n, 256), 256, 0, c->stream>>>(blk + lo, (uint32_t)n, ohist, order + lo);
-      }
       k_inflate_tokens<<<grid_for(n, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
           dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf, lens + lo * LENS_SLOT, bitmap + lo * BITMAP_WORDS,
-          tails + 2 * lo, edges + 32 * lo, st + lo, order ? order + lo : nullptr);
+          tails + 2 * lo, edges + 32 * lo, st + lo);
       if (ns > 1) {
         HIPCHK(c, hipEventRecord(c->slice_ev[si], c->stream));
         HIPCHK(c, hipStreamWaitEvent(rs, c->slice_ev[si], 0));
@@ -1351,10 +1288,9 @@ extern "C" void hbam_split_close(hbam_split_stream* s) {
   delete s;
 }
 
-extern "C" int hbam_columns_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_columns* h) {
-  if (!c || !dv || !h) return HBAM_EINVAL;
-  HIPCHK(c, hipSetDevice(c->device));
-  memset(h, 0, sizeof *h);
+extern "C" void hbam_free_host_columns(hbam_columns* h);
+namespace {
+int columns_to_host_impl(hbam_ctx* c, const hbam_columns* dv, hbam_columns* h) {
   const uint64_t n = dv->n_records;
   h->n_records = n;
   h->status = dv->status;
@@ -1416,6 +1352,21 @@ extern "C" int hbam_columns_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_co
   h->ubuf_len = hi - lo;
   return HBAM_OK;
 }
+}  // namespace
+
+extern "C" int hbam_columns_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_columns* h) {
+  if (!c || !dv || !h) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  memset(h, 0, sizeof *h);
+  const int rc = columns_to_host_impl(c, dv, h);
+  if (rc != HBAM_OK) {
+    // every error return leaves no host arrays behind; the copies already queued
+    // into them must land before they are freed
+    (void)hipStreamSynchronize(c->stream);
+    hbam_free_host_columns(h);
+  }
+  return rc;
+}
 
 extern "C" void hbam_free_host_columns(hbam_columns* h) {
   if (!h) return;
@@ -1440,14 +1391,14 @@ struct GuessWork {
   uint8_t* scratch;
   uint8_t* lens;
   uint8_t* bufs;
-  int64_t *beg, *end, *out;
+  int64_t *beg, *end, *out, *wlen;
+  uint64_t* wptr;
   int32_t* err;
 };
 int guess_work(hbam_ctx* c, uint64_t k, GuessWork* w) {
-  // carve from B_REL / B_LENS / B_PARTIAL-like dedicated slots: use B_UBUF for scratch
   int rc;
   uint8_t* base;
-  const uint64_t per = 65536 + LENS_SLOT + 8 + 8 * 3 + 4;
+  const uint64_t per = 65536 + LENS_SLOT + 8 + 8 * 5 + 4;
   if ((rc = ensure(c, B_G_WORK, k * per + 4096, &base))) return rc;
   w->scratch = base;
   w->lens = base + k * 65536;
@@ -1457,7 +1408,9 @@ int guess_work(hbam_ctx* c, uint64_t k, GuessWork* w) {
   w->beg = (int64_t*)q;
   w->end = w->beg + k;
   w->out = w->end + k;
-  w->err = (int32_t*)(w->out + k);
+  w->wlen = w->out + k;
+  w->wptr = (uint64_t*)(w->wlen + k);
+  w->err = (int32_t*)(w->wptr + k);
   return HBAM_OK;
 }
 
@@ -1471,15 +1424,14 @@ struct GuessCache {
   int32_t* cst = nullptr;
   uint32_t* ccrc = nullptr;
 };
-int build_guess_cache(hbam_ctx* c, const uint8_t* d, uint64_t file_len, const int64_t* dbeg,
-                      const int64_t* dend, uint64_t k, GuessCache* gc) {
+int build_guess_cache(hbam_ctx* c, const GuessWork& w, uint64_t k, GuessCache* gc) {
   int rc;
   uint64_t* slots;
   uint32_t* cisz;
   if ((rc = ensure(c, B_G_CN, k + 1, &gc->cn))) return rc;
   if ((rc = ensure(c, B_G_CBASE, k + 1, &gc->cbase))) return rc;
   if ((rc = ensure(c, B_G_SLOTS, k * GC_CAP, &slots))) return rc;
-  k_guess_cands<<<(uint32_t)k, 256, 0, c->stream>>>(d, (int64_t)file_len, dbeg, dend, gc->cn, slots);
+  k_guess_cands<<<(uint32_t)k, 256, 0, c->stream>>>(w.wptr, w.wlen, w.beg, w.end, gc->cn, slots);
   HIPCHK(c, hipGetLastError());
   // windows over the cap contribute no cached blocks: clamp the counts for the scan
   uint32_t* cn_eff;
@@ -1490,7 +1442,7 @@ int build_guess_cache(hbam_ctx* c, const uint8_t* d, uint64_t file_len, const in
   if ((rc = ensure(c, B_G_CPOS, ncand + 1, &gc->cpos))) return rc;
   if ((rc = ensure(c, B_G_CBLK, ncand + 1, &gc->cblk))) return rc;
   if ((rc = ensure(c, B_G_CISZ, ncand + 1, &cisz))) return rc;
-  k_guess_cand_blocks<<<(uint32_t)k, 64, 0, c->stream>>>(d, (int64_t)file_len, (uint32_t)k, gc->cn,
+  k_guess_cand_blocks<<<(uint32_t)k, 64, 0, c->stream>>>(w.wptr, w.wlen, w.beg, w.end, (uint32_t)k, gc->cn,
                                                         gc->cbase, slots, gc->cpos, gc->cblk, cisz);
   HIPCHK(c, hipGetLastError());
   uint64_t utotal = 0;
@@ -1499,38 +1451,35 @@ int build_guess_cache(hbam_ctx* c, const uint8_t* d, uint64_t file_len, const in
   if ((rc = ensure(c, B_G_CUBUF, utotal + UBUF_SLACK, &gc->cubuf))) return rc;
   if ((rc = ensure(c, B_G_CST, ncand + 1, &gc->cst))) return rc;
   if ((rc = ensure(c, B_G_CCRC, ncand + 1, &gc->ccrc))) return rc;
+  // block records carry device addresses (windows live in different buffers): comp = null
   if (ncand)
-    if ((rc = inflate_blocks(c, d, gc->cblk, ncand, gc->cuoff, gc->cubuf, gc->cst, true, gc->ccrc)))
+    if ((rc = inflate_blocks(c, nullptr, gc->cblk, ncand, gc->cuoff, gc->cubuf, gc->cst, true, gc->ccrc)))
       return rc;
   return HBAM_OK;
 }
 
-}  // namespace
+// The window a guesser reads (BAMSplitGuesser.java:114-125 / BGZFSplitGuesser.java:62-63):
+// min((int)(end - beg), cap) bytes from beg, cut at the end of the file.
+uint64_t window_len(uint64_t file_len, int64_t beg, int64_t end, int64_t cap) {
+  int32_t want = (int32_t)(end - beg);
+  if (want > cap) want = (int32_t)cap;
+  if (want <= 0 || beg < 0 || (uint64_t)beg > file_len) return 0;
+  const uint64_t avail = file_len - (uint64_t)beg;
+  return avail < (uint64_t)want ? avail : (uint64_t)want;
+}
 
-extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device, uint64_t file_len,
-                                const int64_t* beg, const int64_t* end, uint64_t k, int32_t n_ref,
-                                int64_t* out, int32_t* err) {
-  if (!c || !file || (k && (!beg || !end || !out || !err))) return HBAM_EINVAL;
-  HIPCHK(c, hipSetDevice(c->device));
-  if (k == 0) return HBAM_OK;
-  const uint8_t* d;
-  int rc = stage_comp(c, file, on_device, file_len, &d);
-  if (rc) return rc;
+// k BAM guesses over device windows (wptr[i]: device address of file byte beg[i], wlen[i]
+// bytes there), in launches of c->guess_batch.
+int guess_run(hbam_ctx* c, const uint64_t* wptr, const int64_t* wlen, const int64_t* beg,
+              const int64_t* end, uint64_t k, int32_t n_ref, int64_t* out, int32_t* err) {
   // Initial ByteBuffer of BAMSplitGuesser(ss, conf): the ctor reads the file magic into it
-  // (:85-87).  Only windows shorter than 4 bytes could observe a stale buffer carried over
-  // from a previous guess, and those always return `end` (the XLEN seek at p0+10 fails),
-  // so guesses are independent.
-  uint8_t magic[8] = {0};
-  {
-    const uint64_t n4 = std::min<uint64_t>(file_len, 4);
-    if (n4) {
-      HIPCHK(c, hipMemcpyAsync(c->pinned_small, d, n4, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      memcpy(magic, c->pinned_small, n4);
-    }
-  }
+  // (:85-87) and throws unless it is 1f 8b 08 04.  Only windows shorter than 4 bytes could
+  // observe a stale buffer carried over from a previous guess, and those always return `end`
+  // (the XLEN seek at p0+10 fails), so guesses are independent.
+  const uint8_t magic[8] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0};
   HIPCHK(c, hipEventRecord(c->ev[9], c->stream));
   uint64_t batch = c->guess_batch;
+  int rc;
   for (uint64_t g0 = 0; g0 < k;) {
     const uint64_t kb = std::min(batch, k - g0);
     GuessWork w;
@@ -1546,8 +1495,10 @@ extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device,
     HIPCHK(c, hipMemcpyAsync(w.bufs, ib.data(), kb * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(w.beg, beg + g0, kb * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(w.end, end + g0, kb * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(w.wptr, wptr + g0, kb * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(w.wlen, wlen + g0, kb * 8, hipMemcpyHostToDevice, c->stream));
     GuessCache gc;
-    if ((rc = build_guess_cache(c, d, file_len, w.beg, w.end, kb, &gc))) {
+    if ((rc = build_guess_cache(c, w, kb, &gc))) {
       if (rc == HBAM_ENOMEM && kb > 1) {
         batch = (kb + 1) / 2;
         continue;
@@ -1555,7 +1506,7 @@ extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device,
       return rc;
     }
     k_guess_bam_wave<<<(uint32_t)kb, 64, 0, c->stream>>>(
-        d, (int64_t)file_len, w.beg, w.end, (uint32_t)kb, n_ref, w.scratch, w.lens, w.bufs, w.out,
+        w.wptr, w.wlen, w.beg, w.end, (uint32_t)kb, n_ref, w.scratch, w.lens, w.bufs, w.out,
         w.err, gc.cn, gc.cbase, gc.cpos, gc.cblk, gc.cuoff, gc.cubuf, gc.cst, gc.ccrc);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(out + g0, w.out, kb * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1570,6 +1521,99 @@ extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device,
   return HBAM_OK;
 }
 
+// Windows of a whole file: views into a device-resident file, or (host file) the windows
+// gathered on the host and staged alone — no guess call stages the file.
+int file_windows(hbam_ctx* c, const uint8_t* file, int on_device, uint64_t file_len, const int64_t* beg,
+                 const int64_t* end, uint64_t k, int64_t cap, std::vector<uint64_t>* wptr,
+                 std::vector<int64_t>* wlen) {
+  wptr->resize(k);
+  wlen->resize(k);
+  std::vector<uint64_t> woff(k + 1, 0);
+  for (uint64_t i = 0; i < k; ++i) {
+    (*wlen)[i] = (int64_t)window_len(file_len, beg[i], end[i], cap);
+    woff[i + 1] = woff[i] + (uint64_t)(*wlen)[i];
+  }
+  if (on_device) {
+    for (uint64_t i = 0; i < k; ++i)
+      (*wptr)[i] = (uint64_t)(uintptr_t)(file + ((*wlen)[i] ? beg[i] : 0));
+    return HBAM_OK;
+  }
+  uint8_t* dw;
+  int rc;
+  if ((rc = ensure(c, B_G_WIN, woff[k] + 64, &dw))) return rc;
+  for (uint64_t i = 0; i < k; ++i) {
+    if ((*wlen)[i])
+      HIPCHK(c, hipMemcpyAsync(dw + woff[i], file + beg[i], (size_t)(*wlen)[i], hipMemcpyHostToDevice, c->stream));
+    (*wptr)[i] = (uint64_t)(uintptr_t)(dw + woff[i]);
+  }
+  return HBAM_OK;
+}
+
+// Caller-gathered windows: window i = windows[win_off[i], win_off[i+1]), which must be exactly
+// the bytes the guesser reads (window_len); staged to the device when on the host.
+int caller_windows(hbam_ctx* c, const uint8_t* windows, int on_device, const uint64_t* win_off,
+                   uint64_t file_len, const int64_t* beg, const int64_t* end, uint64_t k, int64_t cap,
+                   std::vector<uint64_t>* wptr, std::vector<int64_t>* wlen) {
+  wptr->resize(k);
+  wlen->resize(k);
+  if (win_off[0] != 0) return set_err(c, HBAM_EINVAL, "win_off[0] must be 0");
+  for (uint64_t i = 0; i < k; ++i) {
+    const uint64_t want = window_len(file_len, beg[i], end[i], cap);
+    if (win_off[i + 1] < win_off[i] || win_off[i + 1] - win_off[i] != want)
+      return set_err(c, HBAM_EINVAL, "window %llu holds %llu bytes, the guesser reads %llu",
+                     (unsigned long long)i, (unsigned long long)(win_off[i + 1] - win_off[i]),
+                     (unsigned long long)want);
+    (*wlen)[i] = (int64_t)want;
+  }
+  const uint8_t* dw = windows;
+  if (!on_device) {
+    uint8_t* d;
+    int rc;
+    if ((rc = ensure(c, B_G_WIN, win_off[k] + 64, &d))) return rc;
+    if (win_off[k]) HIPCHK(c, hipMemcpyAsync(d, windows, win_off[k], hipMemcpyHostToDevice, c->stream));
+    dw = d;
+  }
+  for (uint64_t i = 0; i < k; ++i) (*wptr)[i] = (uint64_t)(uintptr_t)(dw + win_off[i]);
+  return HBAM_OK;
+}
+
+}  // namespace
+
+extern "C" uint64_t hbam_guess_window_len(uint64_t file_len, int64_t beg, int64_t end) {
+  return window_len(file_len, beg, end, G_MAX_BYTES_READ);
+}
+
+extern "C" uint64_t hbam_guess_bgzf_window_len(uint64_t file_len, int64_t beg, int64_t end) {
+  return window_len(file_len, beg, end, G_BGZF_WINDOW);
+}
+
+extern "C" int hbam_guess_batch(hbam_ctx* c, const uint8_t* file, int on_device, uint64_t file_len,
+                                const int64_t* beg, const int64_t* end, uint64_t k, int32_t n_ref,
+                                int64_t* out, int32_t* err) {
+  if (!c || !file || (k && (!beg || !end || !out || !err))) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (k == 0) return HBAM_OK;
+  std::vector<uint64_t> wp;
+  std::vector<int64_t> wl;
+  int rc = file_windows(c, file, on_device, file_len, beg, end, k, G_MAX_BYTES_READ, &wp, &wl);
+  if (rc) return rc;
+  return guess_run(c, wp.data(), wl.data(), beg, end, k, n_ref, out, err);
+}
+
+extern "C" int hbam_guess_windows(hbam_ctx* c, const uint8_t* windows, int on_device,
+                                  const uint64_t* win_off, uint64_t file_len, const int64_t* beg,
+                                  const int64_t* end, uint64_t k, int32_t n_ref, int64_t* out,
+                                  int32_t* err) {
+  if (!c || (k && (!windows || !win_off || !beg || !end || !out || !err))) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (k == 0) return HBAM_OK;
+  std::vector<uint64_t> wp;
+  std::vector<int64_t> wl;
+  int rc = caller_windows(c, windows, on_device, win_off, file_len, beg, end, k, G_MAX_BYTES_READ, &wp, &wl);
+  if (rc) return rc;
+  return guess_run(c, wp.data(), wl.data(), beg, end, k, n_ref, out, err);
+}
+
 extern "C" int64_t hbam_guess_bam_record_start(hbam_ctx* c, const uint8_t* file, int on_device,
                                                uint64_t file_len, int64_t beg, int64_t end,
                                                int32_t n_ref, int32_t* err) {
@@ -1579,6 +1623,35 @@ extern "C" int64_t hbam_guess_bam_record_start(hbam_ctx* c, const uint8_t* file,
   if (err) *err = rc ? rc : e;
   return out;
 }
+
+namespace {
+int64_t guess_bgzf_run(hbam_ctx* c, uint64_t wptr, int64_t wlen, int64_t beg, int64_t end, int32_t* err) {
+  GuessWork w;
+  int rc = guess_work(c, 1, &w);
+  if (rc) {
+    if (err) *err = rc;
+    return end;
+  }
+  int64_t out = end;
+  int32_t e = HBAM_OK;
+  if (hipMemcpyAsync(w.beg, &beg, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(w.end, &end, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(w.wptr, &wptr, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(w.wlen, &wlen, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    if (err) *err = HBAM_EDEVICE;
+    return end;
+  }
+  k_guess_bgzf<<<1, GUESS_WG, 0, c->stream>>>(w.wptr, w.wlen, w.beg, w.end, 1, w.scratch, w.lens, w.out, w.err);
+  if (hipMemcpyAsync(&out, w.out, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipMemcpyAsync(&e, w.err, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    if (err) *err = HBAM_EDEVICE;
+    return end;
+  }
+  if (err) *err = e;
+  return out;
+}
+}  // namespace
 
 extern "C" int64_t hbam_guess_bgzf_block_start(hbam_ctx* c, const uint8_t* file, int on_device,
                                                uint64_t file_len, int64_t beg, int64_t end,
@@ -1591,65 +1664,46 @@ extern "C" int64_t hbam_guess_bgzf_block_start(hbam_ctx* c, const uint8_t* file,
     if (err) *err = HBAM_EDEVICE;
     return end;
   }
-  const uint8_t* d;
-  int rc = stage_comp(c, file, on_device, file_len, &d);
-  GuessWork w;
-  if (!rc) rc = guess_work(c, 1, &w);
+  std::vector<uint64_t> wp;
+  std::vector<int64_t> wl;
+  const int rc = file_windows(c, file, on_device, file_len, &beg, &end, 1, G_BGZF_WINDOW, &wp, &wl);
   if (rc) {
     if (err) *err = rc;
     return end;
   }
-  int64_t out = end;
-  int32_t e = HBAM_OK;
-  if (hipMemcpyAsync(w.beg, &beg, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-      hipMemcpyAsync(w.end, &end, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
-    if (err) *err = HBAM_EDEVICE;
-    return end;
-  }
-  k_guess_bgzf<<<1, GUESS_WG, 0, c->stream>>>(d, (int64_t)file_len, w.beg, w.end, 1, w.scratch,
-                                              w.lens, w.out, w.err);
-  if (hipMemcpyAsync(&out, w.out, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-      hipMemcpyAsync(&e, w.err, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-      hipStreamSynchronize(c->stream) != hipSuccess) {
-    if (err) *err = HBAM_EDEVICE;
-    return end;
-  }
-  if (err) *err = e;
-  return out;
+  return guess_bgzf_run(c, wp[0], wl[0], beg, end, err);
 }
 
-// BAMInputFormat.addProbabilisticSplits (BAMInputFormat.java:163-224) for one file.
-extern "C" int64_t hbam_probabilistic_splits(hbam_ctx* c, const uint8_t* file, int on_device,
-                                             uint64_t file_len, const uint64_t* beg,
-                                             const uint64_t* end, uint64_t n, uint64_t* v_start,
-                                             uint64_t* v_end) {
-  if (!c || !file || (n && (!beg || !end || !v_start || !v_end))) return HBAM_EINVAL;
-  HIPCHK(c, hipSetDevice(c->device));
-  const uint8_t* d;
-  int rc = stage_comp(c, file, on_device, file_len, &d);
-  if (rc) return rc;
-  hbam_header h;
-  if ((rc = hbam_parse_header(c, d, 1, file_len, &h))) return rc;  // BAMSplitGuesser ctor
-  uint8_t m[4] = {0, 0, 0, 0};
-  if (file_len >= 4) {
-    HIPCHK(c, hipMemcpyAsync(c->pinned_small, d, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    memcpy(m, c->pinned_small, 4);
+extern "C" int64_t hbam_guess_bgzf_window(hbam_ctx* c, const uint8_t* window, int on_device, uint64_t wlen,
+                                          uint64_t file_len, int64_t beg, int64_t end, int32_t* err) {
+  if (!c || (!window && wlen)) {
+    if (err) *err = HBAM_EINVAL;
+    return end;
   }
-  if (file_len < 4 || !(m[0] == 0x1f && m[1] == 0x8b && m[2] == 8 && m[3] == 4))
-    return set_err(c, HBAM_EFORMAT, "Does not seem like a BAM file");
-  std::vector<int64_t> b(n), e(n), g(n);
-  std::vector<int32_t> er(n);
-  for (uint64_t i = 0; i < n; ++i) {
-    b[i] = (int64_t)beg[i];
-    e[i] = (int64_t)end[i];
+  if (hipSetDevice(c->device) != hipSuccess) {
+    if (err) *err = HBAM_EDEVICE;
+    return end;
   }
-  if ((rc = hbam_guess_batch(c, d, 1, file_len, b.data(), e.data(), n, h.n_ref, g.data(), er.data())))
-    return rc;
+  const uint64_t off[2] = {0, wlen};
+  std::vector<uint64_t> wp;
+  std::vector<int64_t> wl;
+  const uint8_t* w = window ? window : (const uint8_t*)off;  // any address for an empty window
+  const int rc = caller_windows(c, w, on_device, off, file_len, &beg, &end, 1, G_BGZF_WINDOW, &wp, &wl);
+  if (rc) {
+    if (err) *err = rc;
+    return end;
+  }
+  return guess_bgzf_run(c, wp[0], wl[0], beg, end, err);
+}
+
+// BAMInputFormat.addProbabilisticSplits (BAMInputFormat.java:163-224) for one file, from the
+// guesses of its FileSplits (the loop after the guesser calls).
+namespace {
+int64_t splits_from_guesses(hbam_ctx* c, const uint64_t* end, uint64_t n, const int64_t* g,
+                            const int32_t* er, uint64_t* v_start, uint64_t* v_end) {
   int64_t out = 0;
   for (uint64_t i = 0; i < n; ++i) {
-    if (er[i]) return set_err(c, er[i], "guesser raised an exception for split %llu",
-                              (unsigned long long)i);
+    if (er[i]) return set_err(c, er[i], "guesser raised an exception for split %llu", (unsigned long long)i);
     const uint64_t aligned_end = end[i] << 16 | 0xffff;
     if (g[i] == (int64_t)end[i]) {
       if (out == 0) return set_err(c, HBAM_EIO, "no reads in first split: bad BAM file or tiny split size?");
@@ -1661,6 +1715,76 @@ extern "C" int64_t hbam_probabilistic_splits(hbam_ctx* c, const uint8_t* file, i
     }
   }
   return out;
+}
+// BAMSplitGuesser(ss, conf) ctor over the file's first head_len bytes: the header (n_ref) and
+// the magic check.  A prefix too short for the header -> HBAM_ETRUNC (read more and retry).
+int guesser_ctor(hbam_ctx* c, const uint8_t* head, int on_device, uint64_t head_len, uint64_t file_len,
+                 int32_t* n_ref) {
+  hbam_header h;
+  int rc = hbam_parse_header(c, head, on_device, head_len, &h);
+  if (rc) return (rc == HBAM_EFORMAT && head_len < file_len) ? set_err(c, HBAM_ETRUNC, "header prefix too short") : rc;
+  uint8_t m[4] = {0, 0, 0, 0};
+  if (head_len >= 4) {
+    if (on_device) {
+      HIPCHK(c, hipMemcpyAsync(c->pinned_small, head, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      memcpy(m, c->pinned_small, 4);
+    } else {
+      memcpy(m, head, 4);
+    }
+  }
+  if (head_len < 4 || !(m[0] == 0x1f && m[1] == 0x8b && m[2] == 8 && m[3] == 4))
+    return set_err(c, HBAM_EFORMAT, "Does not seem like a BAM file");
+  *n_ref = h.n_ref;
+  return HBAM_OK;
+}
+}  // namespace
+
+extern "C" int64_t hbam_probabilistic_splits(hbam_ctx* c, const uint8_t* file, int on_device,
+                                             uint64_t file_len, const uint64_t* beg,
+                                             const uint64_t* end, uint64_t n, uint64_t* v_start,
+                                             uint64_t* v_end) {
+  if (!c || !file || (n && (!beg || !end || !v_start || !v_end))) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  // the header from a growing prefix (the file itself is never staged whole)
+  int32_t n_ref = 0;
+  int rc;
+  for (uint64_t hl = std::min<uint64_t>(file_len, 1 << 20);; hl = std::min<uint64_t>(file_len, 4 * hl)) {
+    rc = guesser_ctor(c, file, on_device, hl, file_len, &n_ref);
+    if (rc != HBAM_ETRUNC || hl == file_len) break;
+  }
+  if (rc) return rc;
+  std::vector<int64_t> b(n), e(n), g(n);
+  std::vector<int32_t> er(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    b[i] = (int64_t)beg[i];
+    e[i] = (int64_t)end[i];
+  }
+  if ((rc = hbam_guess_batch(c, file, on_device, file_len, b.data(), e.data(), n, n_ref, g.data(), er.data())))
+    return rc;
+  return splits_from_guesses(c, end, n, g.data(), er.data(), v_start, v_end);
+}
+
+extern "C" int64_t hbam_probabilistic_splits_windows(hbam_ctx* c, const uint8_t* head, uint64_t head_len,
+                                                     const uint8_t* windows, int on_device,
+                                                     const uint64_t* win_off, uint64_t file_len,
+                                                     const uint64_t* beg, const uint64_t* end, uint64_t n,
+                                                     uint64_t* v_start, uint64_t* v_end) {
+  if (!c || !head || (n && (!windows || !win_off || !beg || !end || !v_start || !v_end))) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  int32_t n_ref = 0;
+  int rc = guesser_ctor(c, head, 0, head_len, file_len, &n_ref);
+  if (rc) return rc;
+  std::vector<int64_t> b(n), e(n), g(n);
+  std::vector<int32_t> er(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    b[i] = (int64_t)beg[i];
+    e[i] = (int64_t)end[i];
+  }
+  if ((rc = hbam_guess_windows(c, windows, on_device, win_off, file_len, b.data(), e.data(), n, n_ref, g.data(),
+                               er.data())))
+    return rc;
+  return splits_from_guesses(c, end, n, g.data(), er.data(), v_start, v_end);
 }
 
 // ---- Sort plugin path (Sort.java:84-188) -----------------------------
@@ -1812,6 +1936,28 @@ extern "C" int hbam_sort_split(hbam_ctx* c, const hbam_columns* dv, hbam_sorted_
   if (dv->status != HBAM_OK) return set_err(c, dv->status, "hbam_sort_split: the decode raised %d", dv->status);
   HIPCHK(c, hipSetDevice(c->device));
   return sort_run(c, dv->key, dv->voffset, dv->block_size, dv->ubuf, dv->rec_off, dv->n_records, out);
+}
+
+extern "C" int hbam_merge_remap(hbam_ctx* c, hbam_columns* dv, const int32_t* ref_map, int32_t n_in,
+                                uint64_t* bad_record) {
+  if (!c || !dv || !bad_record || n_in < 0 || (n_in && !ref_map)) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  *bad_record = ~0ull;
+  const uint64_t n = dv->n_records;
+  if (n == 0) return HBAM_OK;
+  int32_t* dmap;
+  uint64_t* err;
+  int rc;
+  if ((rc = ensure(c, B_M_ERR, 1, &err))) return rc;
+  if ((rc = ensure(c, B_M_MAP, (uint64_t)n_in + 1, &dmap))) return rc;
+  HIPCHK(c, hipMemsetAsync(err, 0xff, 8, c->stream));
+  if (n_in) HIPCHK(c, hipMemcpyAsync(dmap, ref_map, 4ull * n_in, hipMemcpyHostToDevice, c->stream));
+  k_merge_remap<<<grid_for(n, RS_WG), RS_WG, 0, c->stream>>>(dv->ubuf, dv->rec_off, n, dv->ref_id, dv->next_ref_id,
+                                                            dv->key, dv->flag, dv->pos, dmap, n_in,
+                                                            (unsigned long long*)err);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, copy_sync(c, bad_record, err, 8, hipMemcpyDeviceToHost));
+  return HBAM_OK;
 }
 
 extern "C" int hbam_sort_received(hbam_ctx* c, const int64_t* key, const int64_t* voffset,

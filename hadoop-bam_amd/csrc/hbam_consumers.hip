@@ -41,9 +41,25 @@ __device__ __forceinline__ int64_t f4_key0(int32_t ref, int32_t s0) {  // BAMRec
   return (int64_t)((uint64_t)(int64_t)ref << 32) | (int64_t)s0;
 }
 
+// Record layout bounds.  hbam_decode_split hands out a record whose variable fields do not fit
+// its block_size with status OK and layout_ok = 0 (htsjdk decodes those fields lazily and throws
+// only when one is read), so every consumer bounds its reads by the record's own block_size.
+// f4_cigar_ok: name + CIGAR inside the record (what getCigar reads); f4_layout_ok: every field.
+__device__ __forceinline__ bool f4_cigar_ok(const uint8_t* r) {
+  const int64_t bs = f4_ld32(r);
+  return bs >= 32 && 32 + (int64_t)r[12] + 4 * (int64_t)f4_ld16(r + 16) <= bs;
+}
+__device__ __forceinline__ bool f4_layout_ok(const uint8_t* r) {
+  const int64_t bs = f4_ld32(r);
+  const int64_t ls = f4_ld32(r + 20);
+  return bs >= 32 && ls >= 0 && 32 + (int64_t)r[12] + 4 * (int64_t)f4_ld16(r + 16) + (ls + 1) / 2 + ls <= bs;
+}
+
 // ---- Summarize ------------------------------------------------------------------------------
 // Walks one record's CIGAR as SummarizeRecordReader.parseCIGAR (:719-755).  EMIT=false: returns
-// the range count (0xffffffff: an op code > 8, IllegalArgumentException from getCigar).
+// the range count (0xffffffff: an op code > 8, IllegalArgumentException from getCigar;
+// 0xfffffffe: the CIGAR lies outside the record, the runtime exception getCigar's read of it
+// raises in htsjdk; parity unpinned for that exception's class).
 template <bool EMIT>
 __device__ uint32_t f4_ranges(const uint8_t* r, int64_t* key, int32_t* beg, int32_t* end, uint8_t* rev,
                               uint32_t* rec, uint32_t ri) {
@@ -51,6 +67,7 @@ __device__ uint32_t f4_ranges(const uint8_t* r, int64_t* key, int32_t* beg, int3
   const int32_t ref = f4_ld32(r + 4);
   const int32_t start = f4_iadd(f4_ld32(r + 8), 1);
   if ((flag & 4u) || ref < 0 || start < 0) return 0;  // :708-709
+  if (!f4_cigar_ok(r)) return 0xfffffffeu;
   const uint8_t* cig = r + 36 + r[12];
   const uint32_t nc = f4_ld16(r + 16);
   int32_t b = start, e = start;
@@ -112,6 +129,7 @@ __global__ __launch_bounds__(F4_WG) void k_sum_count(const uint8_t* __restrict__
   const uint32_t k = f4_ranges<false>(r, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
   uint32_t kind = 0;
   if (k == 0xffffffffu) kind = 1;
+  else if (k == 0xfffffffeu) kind = 3;
   else if (k == 0 && !((f4_ld16(r + 18) & 4u) || f4_ld32(r + 4) < 0 || f4_iadd(f4_ld32(r + 8), 1) < 0)) kind = 2;
   cnt[i] = kind ? 0u : k;
   if (kind) atomicMin(first_err, (unsigned long long)(i << 2 | kind));
@@ -162,6 +180,15 @@ __global__ __launch_bounds__(F4_WG) void k_name_chunk(const uint8_t* __restrict_
     v = v << 8 | (j < L ? nm[j] : 0u);
   }
   key[i] = (int64_t)(v ^ 0x8000000000000000ull);
+}
+
+// first record whose fields do not fit its block_size (FixMateMapper reads every record's name,
+// the reducer re-encodes every field) -> atomicMin into *first_err
+__global__ __launch_bounds__(F4_WG) void k_layout_check(const uint8_t* __restrict__ ubuf,
+                                                        const uint64_t* __restrict__ rec_off, uint64_t n,
+                                                        unsigned long long* __restrict__ first_err) {
+  const uint64_t i = (uint64_t)blockIdx.x * F4_WG + threadIdx.x;
+  if (i < n && !f4_layout_ok(ubuf + rec_off[i])) atomicMin(first_err, (unsigned long long)i);
 }
 
 __global__ __launch_bounds__(F4_WG) void k_iota(uint64_t n, uint32_t* __restrict__ out) {
@@ -545,7 +572,7 @@ extern "C" int hbam_summarize_ranges(hbam_ctx* c, const hbam_columns* dv, hbam_r
   uint64_t nrec = n;
   if (e != ~0ull) {  // a record raises: the ranges of the records before it, then its exception
     nrec = e >> 2;
-    out->status = (e & 3u) == 1u ? HBAM_EREFID : HBAM_EINDEX;
+    out->status = (e & 3u) == 1u ? HBAM_EREFID : (e & 3u) == 3u ? HBAM_EFORMAT : HBAM_EINDEX;
     HIPCHK(c, copy_sync(c, &total, roff + nrec, 8, hipMemcpyDeviceToHost));
   }
   int64_t* key;
@@ -633,6 +660,19 @@ extern "C" int hbam_fixmate(hbam_ctx* c, const uint8_t* ubuf, const uint64_t* re
       (rc = ensure(c, B_F4_ERR, 2, &err)))
     return rc;
   HIPCHK(c, hipEventRecord(c->ev[13], c->stream));
+  {
+    // a record whose fields overrun its block_size fails the job in the mapper (getReadName /
+    // the lazy field decode throws), before any output: no outputs, SAMFormatException
+    HIPCHK(c, hipMemsetAsync(err, 0xff, 8, c->stream));
+    k_layout_check<<<grid_for(n, F4_WG), F4_WG, 0, c->stream>>>(ubuf, rec_off, n, (unsigned long long*)err);
+    HIPCHK(c, hipGetLastError());
+    uint64_t e = 0;
+    HIPCHK(c, copy_sync(c, &e, err, 8, hipMemcpyDeviceToHost));
+    if (e != ~0ull) {
+      out->status = HBAM_EFORMAT;
+      return HBAM_OK;
+    }
+  }
   if ((rc = hbam_name_order(c, ubuf, rec_off, n, perm))) return rc;
   k_fm_heads<<<grid_for(n, F4_WG), F4_WG, 0, c->stream>>>(ubuf, rec_off, perm, n, head);
   HIPCHK(c, hipGetLastError());

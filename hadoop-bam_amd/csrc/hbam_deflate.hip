@@ -302,27 +302,28 @@ __device__ void df_lengths(const uint32_t* f, uint32_t n, uint32_t maxl, uint8_t
   uint32_t* dep = wt;  // reuse: depth of node i (computed top-down: parents have larger ids)
   dep[ni - 1] = 0;
   for (int i = (int)ni - 2; i >= 0; --i) dep[i] = dep[par[i]] + 1;
-  // bit-length counts with zlib's overflow repair (trees.c gen_bitlen): a leaf deeper than
-  // maxl is moved up beside a shallower leaf, which keeps the Kraft sum exactly 1 (a complete
-  // code: inflate rejects incomplete lit/len and code-length sets)
+  // bit-length counts, limited to maxl with zlib's repair step (trees.c gen_bitlen): leaves
+  // deeper than maxl are clamped to maxl, which over-subscribes the code; each repair step
+  // moves a leaf from the deepest level L < maxl down to L+1 and a leaf from maxl up beside
+  // it, lowering the Kraft sum (in units of 2^-maxl) by exactly one.  The step count is the
+  // Kraft excess itself, so the result is complete (inflate rejects incomplete lit/len and
+  // code-length sets).  (r02 counted only the clamped leaves, which under-repairs any
+  // subtree of 4+ leaves below depth maxl: ADVICE r02.)
   uint32_t cnt[16];
   for (int L = 0; L < 16; ++L) cnt[L] = 0;
-  int overflow = 0;
   for (uint32_t i = 0; i < m; ++i) {
-    uint32_t d = dep[i];
-    if (d > maxl) {
-      d = maxl;
-      ++overflow;
-    }
-    ++cnt[d];
+    const uint32_t d = dep[i];
+    ++cnt[d > maxl ? maxl : d];
   }
-  while (overflow > 0) {
+  uint32_t kraft = 0;
+  for (uint32_t L = 1; L <= maxl; ++L) kraft += cnt[L] << (maxl - L);
+  for (uint32_t excess = kraft - (1u << maxl); excess > 0u && cnt[maxl] > 0u; --excess) {
     uint32_t L = maxl - 1;
-    while (cnt[L] == 0) --L;
+    while (L > 0 && cnt[L] == 0) --L;
+    if (L == 0) break;  // cannot happen for m <= 2^maxl leaves (guard)
     --cnt[L];
     cnt[L + 1] += 2;
     --cnt[maxl];
-    overflow -= 2;
   }
   // lengths by frequency: the least frequent symbols (front of sorted[]) get the longest codes
   uint32_t k = 0;

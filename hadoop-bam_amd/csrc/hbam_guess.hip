@@ -4,7 +4,9 @@
 // so BAMInputFormat.addProbabilisticSplits' per-split loop (BAMInputFormat.java:181-222) and
 // config #3's 10k guesses run as one launch.  The wave runs the reference's state machine
 // over the window W = file[beg, beg+min(end-beg, 262139)) with the same cursor semantics the
-// Java code observes:
+// Java code observes.  Kernels see each guess's window only (the bytes BAMSplitGuesser.java:
+// 114-125 reads): wptr[i] = device address of file byte beg[i] (a view into a device-resident
+// file, or the window a caller gathered), wlen[i] = bytes available there:
 //   * SeekableArrayStream (util/SeekableArrayStream.java:29-58) — one shared position used by
 //     both guessNextBGZFPos and the BlockCompressedInputStream, seek bounds, short reads;
 //   * the persistent 8-byte ByteBuffer `buf` (stale bytes survive short reads);
@@ -353,7 +355,15 @@ __device__ int32_t g_next_bam(Guesser& g, uint64_t cpv, int32_t up, int32_t csiz
 // Candidate blocks of each guess window: every offset of the window (the bytes
 // BAMSplitGuesser's stream can reach, :118-126) that starts with the gzip magic 1f 8b 08 04.
 // One workgroup per window; sorted by rank; count > GC_CAP marks the window uncached.
-__global__ __launch_bounds__(256) void k_guess_cands(const uint8_t* __restrict__ file, int64_t flen,
+// bytes of guess g's window the state machine can reach: min((int)(end-beg), cap, available)
+__device__ __forceinline__ int64_t g_window_total(int64_t b0, int64_t e0, int64_t avail, int32_t cap) {
+  int32_t want = (int32_t)(e0 - b0);  // (int) cast as BAMSplitGuesser.java:118
+  if (want > cap) want = cap;
+  return (want > 0 && b0 >= 0) ? (avail < want ? avail : want) : 0;
+}
+
+__global__ __launch_bounds__(256) void k_guess_cands(const uint64_t* __restrict__ wptr,
+                                                     const int64_t* __restrict__ wlen,
                                                      const int64_t* __restrict__ beg,
                                                      const int64_t* __restrict__ end,
                                                      uint32_t* __restrict__ cn,
@@ -362,14 +372,12 @@ __global__ __launch_bounds__(256) void k_guess_cands(const uint8_t* __restrict__
   __shared__ uint64_t s_p[GC_CAP];
   const uint32_t g = blockIdx.x;
   const int64_t b0 = beg[g];
-  int32_t want = (int32_t)(end[g] - b0);
-  if (want > G_MAX_BYTES_READ) want = G_MAX_BYTES_READ;
-  int64_t total = 0;
-  if (want > 0 && b0 >= 0 && b0 <= flen) total = (flen - b0 < want) ? flen - b0 : want;
+  const int64_t total = g_window_total(b0, end[g], wlen[g], G_MAX_BYTES_READ);
+  const uint8_t* w = (const uint8_t*)wptr[g];
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
   for (int64_t p = threadIdx.x; p + 4 <= total; p += 256) {
-    const uint8_t* q = file + b0 + p;
+    const uint8_t* q = w + p;
     if (q[0] == 0x1f && q[1] == 0x8b && q[2] == 8 && q[3] == 4) {
       const uint32_t k = atomicAdd(&s_n, 1u);
       if (k < GC_CAP) s_p[k] = (uint64_t)(b0 + p);
@@ -398,8 +406,13 @@ __global__ void k_guess_clamp(const uint32_t* __restrict__ cn, uint32_t k, uint3
 }
 
 // Compact the per-window candidate slots and build their block records.  pad = 1 marks a
-// block the cache inflates (whole block inside the file, 26 <= BSIZE+1, ISIZE <= 65536).
-__global__ void k_guess_cand_blocks(const uint8_t* __restrict__ file, int64_t flen, uint32_t k,
+// block the cache inflates (whole block inside the window, 26 <= BSIZE+1, ISIZE <= 65536; the
+// state machine cannot read a block that runs past the window: :94 of gb_read_block).
+// BlockRec.coff is the block's device address (the batched inflate reads comp + coff with
+// comp = nullptr); cpos keeps the absolute file offset the lookups search.
+__global__ void k_guess_cand_blocks(const uint64_t* __restrict__ wptr, const int64_t* __restrict__ wlen,
+                                    const int64_t* __restrict__ beg, const int64_t* __restrict__ end,
+                                    uint32_t k,
                                     const uint32_t* __restrict__ cn, const uint64_t* __restrict__ cbase,
                                     const uint64_t* __restrict__ cpos_slots,
                                     uint64_t* __restrict__ cpos, BlockRec* __restrict__ cblk,
@@ -408,18 +421,22 @@ __global__ void k_guess_cand_blocks(const uint8_t* __restrict__ file, int64_t fl
   if (g >= k) return;
   const uint32_t n = cn[g] <= GC_CAP ? cn[g] : 0u;
   const uint64_t o = cbase[g];
+  const int64_t b0 = beg[g];
+  const int64_t total = g_window_total(b0, end[g], wlen[g], G_MAX_BYTES_READ);
+  const uint8_t* w = (const uint8_t*)wptr[g];
   for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
     const uint64_t p = cpos_slots[(uint64_t)g * GC_CAP + j];
+    const int64_t pr = (int64_t)p - b0;  // window-relative
     BlockRec r;
-    r.coff = p;
+    r.coff = (uint64_t)(uintptr_t)(w + pr);
     r.clen = 0;
     r.isize = 0;
     r.crc = 0;
     r.pad = 0;
-    if ((int64_t)p + 18 <= flen) {
-      const uint32_t bl = (uint32_t)(file[p + 16] | file[p + 17] << 8) + 1u;
-      if (bl >= 26 && (int64_t)(p + bl) <= flen) {
-        const uint8_t* f = file + p + bl - 8;
+    if (pr + 18 <= total) {
+      const uint32_t bl = (uint32_t)(w[pr + 16] | w[pr + 17] << 8) + 1u;
+      if (bl >= 26 && pr + (int64_t)bl <= total) {
+        const uint8_t* f = w + pr + bl - 8;
         const uint32_t crc = (uint32_t)f[0] | (uint32_t)f[1] << 8 | (uint32_t)f[2] << 16 | (uint32_t)f[3] << 24;
         const uint32_t isz = (uint32_t)f[4] | (uint32_t)f[5] << 8 | (uint32_t)f[6] << 16 | (uint32_t)f[7] << 24;
         if (isz <= 65536u) {
@@ -598,7 +615,7 @@ __device__ unsigned int g_gtrace_idx = 0;
   } while (0)
 #define GP_C(i) (void)0
 #endif
-__device__ int64_t g_guess_wave(Guesser& g, const uint8_t* file, int64_t flen, int64_t beg, int64_t end,
+__device__ int64_t g_guess_wave(Guesser& g, const uint8_t* win, int64_t wavail, int64_t beg, int64_t end,
                                 int32_t* err, int32_t* s_mag, uint32_t* s_nmag, uint16_t* s_memo,
                                 uint32_t lane
 #ifdef HBAM_PROF
@@ -609,14 +626,11 @@ __device__ int64_t g_guess_wave(Guesser& g, const uint8_t* file, int64_t flen, i
   uint64_t gq = __builtin_amdgcn_s_memtime();
 #endif
   *err = HBAM_OK;
-  int32_t want = (int32_t)(end - beg);
-  if (want > G_MAX_BYTES_READ) want = G_MAX_BYTES_READ;
-  int64_t total = 0;
-  if (want > 0 && beg >= 0 && beg <= flen) total = (flen - beg < want) ? flen - beg : want;
-  g.in.a = file + ((beg >= 0 && beg <= flen) ? beg : 0);
+  const int64_t total = g_window_total(beg, end, wavail, G_MAX_BYTES_READ);
+  g.in.a = win;
   g.in.len = total;
   g.in.pos = 0;
-  g.bz.wbase = (beg >= 0 && beg <= flen) ? beg : 0;
+  g.bz.wbase = beg >= 0 ? beg : 0;
   g.bz.block_addr = 0;
   g.bz.last_len = 0;
   g.bz.cur_len = -1;
@@ -759,7 +773,8 @@ __device__ int64_t g_guess_wave(Guesser& g, const uint8_t* file, int64_t flen, i
   }
 }
 
-__global__ __launch_bounds__(64) void k_guess_bam_wave(const uint8_t* __restrict__ file, int64_t flen,
+__global__ __launch_bounds__(64) void k_guess_bam_wave(const uint64_t* __restrict__ wptr,
+                                                       const int64_t* __restrict__ wlen,
                                                        const int64_t* __restrict__ beg,
                                                        const int64_t* __restrict__ end, uint32_t k,
                                                        int32_t n_ref, uint8_t* __restrict__ scratch,
@@ -819,13 +834,13 @@ __global__ __launch_bounds__(64) void k_guess_bam_wave(const uint8_t* __restrict
   }
   uint64_t gp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
-  const int64_t r = g_guess_wave(g, file, flen, beg[i], end[i], &e, s_mag, &s_nmag, s_memo, lane, gp);
+  const int64_t r = g_guess_wave(g, (const uint8_t*)wptr[i], wlen[i], beg[i], end[i], &e, s_mag, &s_nmag, s_memo, lane, gp);
   if (g_gprof && lane == 0) {
     gp[0] = __builtin_amdgcn_s_memtime() - t0;  // slot 0: whole guess (listing folded in below)
     for (int q = 0; q < 8; ++q) g_gprof[8 * (uint64_t)i + q] = gp[q];
   }
 #else
-  const int64_t r = g_guess_wave(g, file, flen, beg[i], end[i], &e, s_mag, &s_nmag, s_memo, lane);
+  const int64_t r = g_guess_wave(g, (const uint8_t*)wptr[i], wlen[i], beg[i], end[i], &e, s_mag, &s_nmag, s_memo, lane);
 #endif
   if (lane == 0) {
     out[i] = r;
@@ -835,7 +850,9 @@ __global__ __launch_bounds__(64) void k_guess_bam_wave(const uint8_t* __restrict
 }
 
 // BGZFSplitGuesser.guessNextBGZFBlockStart :51-92 (its own scan :95-148, IOExceptions escape)
-__global__ __launch_bounds__(GUESS_WG) void k_guess_bgzf(const uint8_t* __restrict__ file, int64_t flen,
+constexpr int32_t G_BGZF_WINDOW = 2 * 0xffff - 1;  // BGZFSplitGuesser.java:62-63
+__global__ __launch_bounds__(GUESS_WG) void k_guess_bgzf(const uint64_t* __restrict__ wptr,
+                                                         const int64_t* __restrict__ wlen,
                                                          const int64_t* __restrict__ beg,
                                                          const int64_t* __restrict__ end, uint32_t k,
                                                          uint8_t* __restrict__ scratch,
@@ -849,11 +866,8 @@ __global__ __launch_bounds__(GUESS_WG) void k_guess_bgzf(const uint8_t* __restri
   const uint32_t i = blockIdx.x * GUESS_WG + threadIdx.x;
   if (i >= k) return;
   const int64_t b0 = beg[i], e0 = end[i];
-  int32_t want = (int32_t)(e0 - b0);
-  if (want > 2 * 0xffff - 1) want = 2 * 0xffff - 1;
-  int64_t total = 0;
-  if (want > 0 && b0 >= 0 && b0 <= flen) total = (flen - b0 < want) ? flen - b0 : want;
-  GStream in{file + ((b0 >= 0 && b0 <= flen) ? b0 : 0), total, 0};
+  const int64_t total = g_window_total(b0, e0, wlen[i], G_BGZF_WINDOW);
+  GStream in{(const uint8_t*)wptr[i], total, 0};
   GBcis bz;
   bz.block_addr = 0;
   bz.last_len = 0;
@@ -861,7 +875,7 @@ __global__ __launch_bounds__(GUESS_WG) void k_guess_bgzf(const uint8_t* __restri
   bz.cur_off = 0;
   bz.scratch = scratch + (uint64_t)i * 65536;
   bz.cur = bz.scratch;
-  bz.wbase = (b0 >= 0 && b0 <= flen) ? b0 : 0;
+  bz.wbase = b0 >= 0 ? b0 : 0;
   bz.cache.n = 0;
   bz.s_ll = s_ll + threadIdx.x * 288;
   bz.s_d = s_d + threadIdx.x * 32;

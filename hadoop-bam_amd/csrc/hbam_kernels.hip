@@ -156,15 +156,12 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
                                                                   uint32_t* __restrict__ bitmap,
                                                                   uint32_t* __restrict__ tails,
                                                                   uint8_t* __restrict__ edges,
-                                                                  int32_t* __restrict__ status,
-                                                                  const uint32_t* __restrict__ order) {
+                                                                  int32_t* __restrict__ status) {
   // 320 B of LDS per lane (u8 lit/len + distance symbols): 20 KiB per workgroup -> 8 per CU
   __shared__ uint8_t s_ll[INFLATE_WG * 288];
   __shared__ uint8_t s_d[INFLATE_WG * 32];
-  const uint32_t i = blockIdx.x * INFLATE_WG + threadIdx.x;
-  if (i >= nblk) return;
-  // lane -> block: `order` (blocks by compressed length, longest first) or the file order
-  const uint32_t b = order ? order[i] : i;
+  const uint32_t b = blockIdx.x * INFLATE_WG + threadIdx.x;
+  if (b >= nblk) return;
 #ifdef HBAM_PROF
   const uint64_t pr0 = PROF_RT(), pc0 = PROF_CLK();
 #endif

@@ -209,4 +209,47 @@ __global__ __launch_bounds__(RS_WG) void k_bgzfi_pick(const BlockRec* __restrict
   out[j] = (uint64_t)(int64_t)(int32_t)(uint32_t)p & 0xffffffffffffull;
 }
 
+// Multi-input Sort: SortRecordReader.nextKeyValue (Sort.java:279-295) applies
+// Utils.correctSAMRecordForMerging (cli/Utils.java:286-313) to every record when the inputs'
+// dictionaries differ: refID -> the merged index, next refID too for a paired read (0x1), in
+// the record's bytes (SAMRecordWritable.write encodes them) and the columns, and the key
+// recomputed by BAMRecordReader.getKey when refID changed.  getKey's hash (unmapped records) is
+// over the variable block, which a refID change leaves as it is, so only coordinate keys move.
+// htsjdk's SAMRecord.setReferenceIndex / setMateReferenceIndex resolve the new index against
+// the record's OWN (input) header and throw IllegalArgumentException when it is beyond that
+// dictionary: the first such record -> *first_bad.
+__global__ __launch_bounds__(RS_WG) void k_merge_remap(uint8_t* __restrict__ ubuf,
+                                                       const uint64_t* __restrict__ rec_off, uint64_t n,
+                                                       int32_t* __restrict__ ref_col,
+                                                       int32_t* __restrict__ nref_col,
+                                                       int64_t* __restrict__ key_col,
+                                                       const uint16_t* __restrict__ flag_col,
+                                                       const int32_t* __restrict__ pos_col,
+                                                       const int32_t* __restrict__ map, int32_t n_in,
+                                                       unsigned long long* __restrict__ first_bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * RS_WG + threadIdx.x;
+  if (i >= n) return;
+  auto remap = [&](int32_t x) { return x == -1 ? -1 : (x >= 0 && x < n_in) ? map[x] : n_in; };
+  const int32_t r = ref_col[i], m = nref_col[i];
+  const uint16_t f = flag_col[i];
+  const int32_t nr = remap(r);
+  const int32_t nm = (f & 1u) ? remap(m) : m;
+  if (nr >= n_in || ((f & 1u) && nm >= n_in)) {
+    atomicMin(first_bad, (unsigned long long)i);
+    return;
+  }
+  uint8_t* p = ubuf + rec_off[i];
+  if (nr != r) {
+    for (int k = 0; k < 4; ++k) p[4 + k] = (uint8_t)((uint32_t)nr >> (8 * k));
+    ref_col[i] = nr;
+    const int32_t pos = pos_col[i];
+    if (!(f & 4u) && nr >= 0 && (int32_t)((uint32_t)pos + 1u) >= 0)
+      key_col[i] = (int64_t)((uint64_t)(int64_t)nr << 32 | (uint64_t)(int64_t)pos);
+  }
+  if (nm != m) {
+    for (int k = 0; k < 4; ++k) p[24 + k] = (uint8_t)((uint32_t)nm >> (8 * k));
+    nref_col[i] = nm;
+  }
+}
+
 }  // namespace hbam

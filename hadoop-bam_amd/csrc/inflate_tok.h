@@ -28,7 +28,7 @@
 
 namespace hbam {
 
-#ifdef HBAM_PROF
+#if defined(HBAM_PROF) && !defined(HBAM_PROF_NOSTAMP)
 // Profiling build only: wave-level cycles per region of the Huffman pass (tools/prof_regions.py)
 #define TOK_PT(i)                                   \
   do {                                              \
@@ -1038,6 +1038,12 @@ leave:
 done:
   sink.finish();
   *produced = op;
+#ifdef HBAM_PROF
+  // decoder state at exit (tools/diag_inflate_build.py)
+  pc[1] = in.consumed;
+  pc[2] = in.bc | in.nv << 8 | in.rd << 16;
+  pc[3] = it;
+#endif
   return rc;
 }
 

@@ -49,6 +49,8 @@ EXPORTS = [
     "hbam_split_stats", "hbam_split_close", "hbam_device_alloc", "hbam_sort_split",
     "hbam_sort_partition", "hbam_sort_received", "hbam_bgzf_bound", "hbam_bgzf_compress",
     "hbam_summarize_ranges", "hbam_name_order", "hbam_fixmate", "hbam_download",
+    "hbam_guess_window_len", "hbam_guess_windows", "hbam_guess_bgzf_window_len",
+    "hbam_guess_bgzf_window", "hbam_probabilistic_splits_windows", "hbam_merge_remap",
 ]
 
 
@@ -164,6 +166,14 @@ def load(path=None):
                                                     C.c_int64, _i32p]),
         "hbam_probabilistic_splits": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, vp, vp,
                                                   C.c_uint64, vp, vp]),
+        "hbam_guess_window_len": (C.c_uint64, [C.c_uint64, C.c_int64, C.c_int64]),
+        "hbam_guess_bgzf_window_len": (C.c_uint64, [C.c_uint64, C.c_int64, C.c_int64]),
+        "hbam_guess_windows": (C.c_int, [vp, vp, C.c_int, vp, C.c_uint64, vp, vp, C.c_uint64,
+                                         C.c_int32, vp, vp]),
+        "hbam_guess_bgzf_window": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_uint64, C.c_int64,
+                                               C.c_int64, _i32p]),
+        "hbam_probabilistic_splits_windows": (C.c_int64, [vp, vp, C.c_uint64, vp, C.c_int, vp,
+                                                          C.c_uint64, vp, vp, C.c_uint64, vp, vp]),
         "hbam_sort_keys": (C.c_int, [vp, vp, C.c_uint64, vp, vp]),
         "hbam_gather_records": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, vp, C.c_uint64, vp,
                                           C.POINTER(C.c_uint64)]),
@@ -182,6 +192,7 @@ def load(path=None):
         "hbam_sort_split": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(SortedRunC)]),
         "hbam_sort_partition": (C.c_int, [vp, C.POINTER(SortedRunC), vp, C.c_uint32, vp, vp]),
         "hbam_sort_received": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, C.POINTER(SortedRunC)]),
+        "hbam_merge_remap": (C.c_int, [vp, C.POINTER(Columns), vp, C.c_int32, C.POINTER(C.c_uint64)]),
         "hbam_bgzf_bound": (C.c_uint64, [C.c_uint64, C.c_uint32]),
         "hbam_summarize_ranges": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(RangesC)]),
         "hbam_name_order": (C.c_int, [vp, vp, vp, C.c_uint64, vp]),
@@ -263,6 +274,13 @@ class Context:
         """(pointer, length, on_device, keepalive) for bytes / numpy / torch cuda tensor."""
         if hasattr(data, "data_ptr") and hasattr(data, "is_cuda"):
             if data.is_cuda:
+                # libhbam reads the raw pointer on its own stream: the bytes must be one dense
+                # run, and whatever torch is still producing into them (a torch.cat, a .to(dev),
+                # an all_to_all) must be finished first (ADVICE r02)
+                if not data.is_contiguous():
+                    raise ValueError("device input must be contiguous")
+                import torch
+                torch.cuda.current_stream(data.device).synchronize()
                 return C.c_void_p(data.data_ptr()), data.numel() * data.element_size(), 1, data
             a = data.numpy()
         elif isinstance(data, np.ndarray):
@@ -411,6 +429,49 @@ class Context:
         rc = self.L.hbam_guess_batch(self.h, p, dev, n, beg.ctypes.data, end.ctypes.data, k,
                                      n_ref, out.ctypes.data, err.ctypes.data)
         return rc, out[:k], err[:k]
+
+    def guess_window_len(self, file_len, beg, end):
+        return int(self.L.hbam_guess_window_len(int(file_len), int(beg), int(end)))
+
+    def guess_bgzf_window_len(self, file_len, beg, end):
+        return int(self.L.hbam_guess_bgzf_window_len(int(file_len), int(beg), int(end)))
+
+    def guess_windows(self, windows, win_off, file_len, beg, end, n_ref):
+        """hbam_guess_windows: windows = the k guess windows concatenated (win_off: k+1)."""
+        p, n, dev, keep = self._ptr(windows)
+        beg = np.ascontiguousarray(beg, np.int64)
+        end = np.ascontiguousarray(end, np.int64)
+        win_off = np.ascontiguousarray(win_off, np.uint64)
+        k = len(beg)
+        out = np.zeros(max(k, 1), np.int64)
+        err = np.zeros(max(k, 1), np.int32)
+        rc = self.L.hbam_guess_windows(self.h, p, dev, win_off.ctypes.data, int(file_len), beg.ctypes.data,
+                                       end.ctypes.data, k, n_ref, out.ctypes.data, err.ctypes.data)
+        return rc, out[:k], err[:k]
+
+    def guess_bgzf_window(self, window, file_len, beg, end):
+        p, n, dev, keep = self._ptr(window)
+        e = C.c_int32(0)
+        r = self.L.hbam_guess_bgzf_window(self.h, p, dev, n, int(file_len), int(beg), int(end), C.byref(e))
+        return r, e.value
+
+    def probabilistic_splits_windows(self, head, windows, win_off, file_len, beg, end):
+        hp, hn, hdev, hkeep = self._ptr(head)
+        if hdev:
+            raise ValueError("the header prefix is a host buffer")
+        p, n, dev, keep = self._ptr(windows)
+        beg = np.ascontiguousarray(beg, np.uint64)
+        end = np.ascontiguousarray(end, np.uint64)
+        win_off = np.ascontiguousarray(win_off, np.uint64)
+        k = len(beg)
+        vs = np.zeros(max(k, 1), np.uint64)
+        ve = np.zeros(max(k, 1), np.uint64)
+        r = self.L.hbam_probabilistic_splits_windows(self.h, hp, hn, p, dev, win_off.ctypes.data, int(file_len),
+                                                     beg.ctypes.data, end.ctypes.data, k, vs.ctypes.data,
+                                                     ve.ctypes.data)
+        if r < 0:
+            return r, None, None
+        return r, vs[:r], ve[:r]
 
     def guess_bgzf_block_start(self, data, beg, end):
         p, n, dev, keep = self._ptr(data)

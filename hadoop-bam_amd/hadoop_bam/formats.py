@@ -207,37 +207,89 @@ def _read_file(path):
         return f.read()
 
 
+class SeekableFile:
+    """SeekableStream over a path, an open binary file or an in-memory buffer: only the byte
+    ranges asked for are read (a guess reads its window, getSplits its FileSplits' windows and
+    the header prefix — never the whole file)."""
+
+    def __init__(self, src):
+        self._f, self._own, self._buf = None, False, None
+        if isinstance(src, SeekableFile):
+            self._f, self._buf, self.length = src._f, src._buf, src.length
+        elif isinstance(src, (bytes, bytearray, memoryview, np.ndarray)):
+            self._buf = np.frombuffer(src, np.uint8) if not isinstance(src, np.ndarray) else src
+            self.length = len(self._buf)
+        elif hasattr(src, "read") and hasattr(src, "seek"):
+            self._f = src
+            self.length = src.seek(0, os.SEEK_END)
+        else:
+            self._f = open(src, "rb")
+            self._own = True
+            self.length = os.path.getsize(src)
+
+    def read_at(self, off, n):
+        n = max(0, min(int(n), self.length - int(off)))
+        if n == 0:
+            return b""
+        if self._buf is not None:
+            return bytes(self._buf[off:off + n])
+        self._f.seek(off)
+        return self._f.read(n)
+
+    def close(self):
+        if self._own and self._f is not None:
+            self._f.close()
+        self._f = None
+
+
+def read_header_prefix(ss, ctx):
+    """SAMHeaderReader.readSAMHeaderFrom over a growing prefix of the stream (the header is
+    usually one or two BGZF blocks) -> (header dict, prefix bytes)."""
+    n = min(ss.length, 1 << 20)
+    while True:
+        head = ss.read_at(0, n)
+        h = ctx.parse_header(head)
+        if isinstance(h, dict) or n >= ss.length:
+            return h, head
+        n = min(ss.length, 4 * n)
+
+
 # ---- split guessers ------------------------------------------------------------------
 class BAMSplitGuesser:
-    """BAMSplitGuesser.java:50-398 (the guess runs as one device lane)."""
+    """BAMSplitGuesser.java:50-398 (one device wave per guess).  A guess reads only its window
+    (hbam_guess_window_len bytes at beg, :114-125) from the stream and hands it to
+    hbam_guess_windows."""
 
     def __init__(self, ss, conf=None, header_stream=None):
-        self.data = _read_file(ss)
+        self.ss = SeekableFile(ss)
         self.conf = conf or Configuration()
         self.ctx = context(conf)
-        h = self.ctx.parse_header(self.data if header_stream is None else _read_file(header_stream))
+        h, _ = read_header_prefix(self.ss if header_stream is None else SeekableFile(header_stream), self.ctx)
         if isinstance(h, int):
             raise_for(h, "cannot read SAM header")
         self.n_ref = h["n_ref"]
-        if header_stream is None and bytes(self.data[:4]) != b"\x1f\x8b\x08\x04":
+        if header_stream is None and self.ss.read_at(0, 4) != b"\x1f\x8b\x08\x04":
             raise SAMFormatException("Does not seem like a BAM file")
 
     def guessNextBAMRecordStart(self, beg, end):
-        rc, out, err = self.ctx.guess_batch(self.data, [beg], [end], self.n_ref)
+        wl = self.ctx.guess_window_len(self.ss.length, beg, end)
+        w = self.ss.read_at(beg, wl)
+        rc, out, err = self.ctx.guess_windows(w, [0, wl], self.ss.length, [beg], [end], self.n_ref)
         raise_for(rc, self.ctx.last_error())
         raise_for(int(err[0]), "exception escaped the guesser")
         return int(out[0])
 
 
 class BGZFSplitGuesser:
-    """util/BGZFSplitGuesser.java:30-148."""
+    """util/BGZFSplitGuesser.java:30-148; a guess reads its one window (:62-63)."""
 
     def __init__(self, inp, conf=None):
-        self.data = _read_file(inp)
+        self.ss = SeekableFile(inp)
         self.ctx = context(conf)
 
     def guessNextBGZFBlockStart(self, beg, end):
-        r, e = self.ctx.guess_bgzf_block_start(self.data, beg, end)
+        wl = self.ctx.guess_bgzf_window_len(self.ss.length, beg, end)
+        r, e = self.ctx.guess_bgzf_window(self.ss.read_at(beg, wl), self.ss.length, beg, end)
         raise_for(e, "exception escaped the guesser")
         return int(r)
 
@@ -891,8 +943,10 @@ class BAMInputFormat:
         return j_end
 
     def _add_probabilistic_splits(self, splits, i, out, cfg):  # :163-224
+        """The guesses of one file's FileSplits as one hbam_probabilistic_splits_windows call:
+        the header prefix and each split's guess window are read from the file, nothing else."""
         path = splits[i].getPath()
-        data = _read_file(path)
+        ss = SeekableFile(path)
         ctx = context(cfg)
         j = i
         beg, end = [], []
@@ -900,7 +954,18 @@ class BAMInputFormat:
             beg.append(splits[j].getStart())
             end.append(splits[j].getStart() + splits[j].getLength())
             j += 1
-        n, vs, ve = ctx.probabilistic_splits(data, beg, end)
+        lens = [ctx.guess_window_len(ss.length, b, e) for b, e in zip(beg, end)]
+        win_off = np.zeros(len(lens) + 1, np.uint64)
+        win_off[1:] = np.cumsum(lens)
+        windows = b"".join(ss.read_at(b, n) for b, n in zip(beg, lens))
+        hn = min(ss.length, 1 << 20)
+        while True:
+            n, vs, ve = ctx.probabilistic_splits_windows(ss.read_at(0, hn), windows, win_off,
+                                                         ss.length, beg, end)
+            if n != _lib.HBAM_ETRUNC or hn >= ss.length:
+                break
+            hn = min(ss.length, 4 * hn)
+        ss.close()
         if n < 0:
             raise_for(int(n), ctx.last_error())
         # each virtual split carries the locations of the FileSplit whose guess opened it

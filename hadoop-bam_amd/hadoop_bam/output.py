@@ -224,8 +224,12 @@ def merge_sam_into(out_path, directory, base_prefix, base_postfix, header, work_
     """cli/Utils.mergeSAMInto (:333-356) for BAM: the merged header through its own BGZF
     stream (SAMOutputPreparer), the work files (mergeInto :194-229: glob
     prefix+work+postfix-[0-9]{6}*, in name order) copied byte for byte and deleted, then the
-    BGZF EOF block."""
+    BGZF EOF block.  `header` is getSAMHeaderMerger(conf).getMergedHeader() (:348-349): a
+    SAMFileHeader, or the inputs' headers (a list), merged here with coordinate order (Sort)."""
     import fnmatch
+    if isinstance(header, (list, tuple)):
+        from .sort import SamFileHeaderMerger
+        header = SamFileHeaderMerger("coordinate", header).getMergedHeader() if len(header) > 1 else header[0]
     pat = base_prefix + work_filename + base_postfix + "-" + "[0-9]" * 6 + "*"
     parts = sorted(f for f in os.listdir(directory) if fnmatch.fnmatchcase(f, pat))
     with open(out_path, "wb") as outs:

@@ -201,3 +201,157 @@ def sort_sharded(run, dist, ops, all_gather_fn):
     """Steps 2-4 for one rank: split points, exchange, local stable sort."""
     sp = choose_split_points(run.keys, dist.get_world_size(), all_gather_fn)
     return exchange(run, sp, dist, ops)
+
+
+# ---- several inputs: Utils.getSAMHeaderMerger / correctSAMRecordForMerging -------------------
+class SAMException(RuntimeError):
+    """htsjdk.samtools.SAMException"""
+
+
+def _header_records(text, tag):
+    """(ID, attribute set) of every @RG / @PG line of a header text, in order."""
+    out = []
+    for ln in text.split(b"\n"):
+        if ln.startswith(tag + b"\t"):
+            f = ln.split(b"\t")[1:]
+            rid = next((x[3:] for x in f if x.startswith(b"ID:")), b"")
+            out.append((rid, frozenset(x for x in f if not x.startswith(b"ID:"))))
+    return out
+
+
+def merge_sequences(into, frm):
+    """SamFileHeaderMerger.mergeSequences (htsjdk 1.131, restated from its published behaviour:
+    parity unpinned).  Sequences of `frm` missing from `into` are held and inserted before the
+    next sequence both share; one shared sequence earlier than a previous shared one cannot be
+    placed: SAMException.  Entries are (name, length); an existing entry keeps its length."""
+    result = list(into)
+    names = [n for n, _ in result]
+    holder, prevloc, prev = [], -1, None
+    for rec in frm:
+        loc = names.index(rec[0]) if rec[0] in names else -1
+        if loc == -1:
+            holder.append(rec)
+        elif prevloc > loc:
+            raise SAMException("Cannot merge sequence dictionaries because sequence %s and %s are in "
+                               "different orders in two input sequence dictionaries."
+                               % (rec[0].decode(errors="replace"), prev[0].decode(errors="replace")))
+        else:
+            result[loc:loc] = holder
+            names[loc:loc] = [n for n, _ in holder]
+            prevloc = loc + len(holder)
+            prev = rec
+            holder = []
+    result += holder
+    return result
+
+
+def _same_dictionary(a, b):
+    """SequenceUtil.assertSequenceListsEqual: same size, names, and lengths (0 = unknown)."""
+    return len(a) == len(b) and all(x[0] == y[0] and (x[1] == y[1] or 0 in (x[1], y[1])) for x, y in zip(a, b))
+
+
+class SamFileHeaderMerger:
+    """new SamFileHeaderMerger(sortOrder, headers, true) as Utils.getSAMHeaderMerger builds it
+    (cli/Utils.java:252-283).  htsjdk 1.131 is absent here, so its behaviour is restated (parity
+    unpinned): the dictionary is merged only when the inputs' dictionaries differ
+    (hasMergedSequenceDictionary), by mergeSequences over the inputs in order; the merged header
+    holds the merged dictionary, the inputs' @RG / @PG records (identical records from several
+    inputs kept once) and comments, sort order `sort_order`.
+
+    Read / program group ID collisions (one ID with different attributes in two inputs) are not
+    supported: correctSAMRecordForMerging then rewrites RG tags through the PROGRAM-group table
+    (Utils.java:318-323, getProgramGroupId for RG), which drops or NPEs in htsjdk; this raises
+    NotImplementedError instead of imitating that."""
+
+    def __init__(self, sort_order, headers):
+        self.headers = list(headers)
+        dicts = [h.refs for h in self.headers]
+        if all(_same_dictionary(dicts[0], d) for d in dicts[1:]):
+            self.merged_refs = list(dicts[0])
+            self.has_merged_sequence_dictionary = False
+        else:
+            m = []
+            for d in dicts:
+                m = merge_sequences(m, d)
+            self.merged_refs = m
+            self.has_merged_sequence_dictionary = True
+        names = {n: i for i, (n, _) in enumerate(self.merged_refs)}
+        # createSequenceMapping: input index -> merged index, by name
+        self.ref_maps = [np.array([names[n] for n, _ in d], np.int32) for d in dicts]
+        for tag in (b"@RG", b"@PG"):
+            seen = {}
+            for h in self.headers:
+                for rid, attrs in _header_records(h.text, tag):
+                    if seen.setdefault(rid, attrs) != attrs:
+                        raise NotImplementedError(
+                            "%s ID %r differs between inputs: the reference remaps RG tags through the "
+                            "program-group table (cli/Utils.java:314-323); not supported"
+                            % (tag.decode(), rid))
+        self.sort_order = sort_order
+
+    def getMergedHeader(self):
+        from .output import SAMFileHeader
+        lines = [b"@HD\tVN:1.4\tSO:" + self.sort_order.encode()]
+        for n, ln in self.merged_refs:
+            lines.append(b"@SQ\tSN:" + n + b"\tLN:" + str(ln).encode())
+        for tag in (b"@RG", b"@PG"):
+            done = set()
+            recs = []
+            for h in self.headers:
+                for ln in h.text.split(b"\n"):
+                    if ln.startswith(tag + b"\t") and ln not in done:
+                        done.add(ln)
+                        recs.append(ln)
+            if tag == b"@RG":  # mergeReadGroups sorts by ID
+                recs.sort(key=lambda x: next((f[3:] for f in x.split(b"\t") if f.startswith(b"ID:")), b""))
+            lines += recs
+        for h in self.headers:
+            lines += [ln for ln in h.text.split(b"\n") if ln.startswith(b"@CO")]
+        return SAMFileHeader(b"\n".join(lines) + b"\n", self.merged_refs)
+
+
+def correct_for_merging(ctx, cols, merger, input_index):
+    """SortRecordReader.nextKeyValue's Utils.correctSAMRecordForMerging over a decoded split
+    (device hbam_columns, modified in place) of input `input_index` (hbam_merge_remap)."""
+    if not merger.has_merged_sequence_dictionary:
+        return
+    m = np.ascontiguousarray(merger.ref_maps[input_index], np.int32)
+    bad = C.c_uint64(0)
+    rc = ctx.L.hbam_merge_remap(ctx.h, C.byref(cols), C.c_void_p(m.ctypes.data), len(m), C.byref(bad))
+    if rc:
+        raise RuntimeError("hbam_merge_remap failed (%d): %s" % (rc, ctx.last_error()))
+    if bad.value != (1 << 64) - 1:
+        raise ValueError("Reference index not found in sequence dictionary (record %d of input %d: "
+                         "SAMRecord.setReferenceIndex against the input's header)" % (bad.value, input_index))
+
+
+def sort_inputs(ctx, inputs, ops=None, sort_order="coordinate"):
+    """Sort.run over several BAM inputs on one GPU (Sort.java:84-188 with
+    HEADERMERGER_INPUTS = every input, :111-113): each input decoded as one split, corrected for
+    the merged header, sorted on the device; the runs, concatenated in input order, stably
+    sorted once more.  Returns (merged header, SortedRun): the total order (key, input index,
+    voffset) — the documented tie-break."""
+    from .output import read_sam_header
+    import torch
+    ops = ops or HipSortOps(ctx)
+    heads = [read_sam_header(d, ctx) for d in inputs]
+    merger = SamFileHeaderMerger(sort_order, heads)
+    runs = []
+    for i, data in enumerate(inputs):
+        h = ctx.parse_header(data)
+        if not isinstance(h, dict):
+            raise RuntimeError("cannot read the header of input %d (%d)" % (i, h))
+        n = len(data) if not hasattr(data, "numel") else data.numel()
+        rc, cols = ctx.decode_split_device(data, h["first_voffset"], (n << 16) | 0xffff, h["n_ref"])
+        if rc or cols.status:
+            raise RuntimeError("decode of input %d failed rc=%d status=%d: %s" % (i, rc, cols.status, ctx.last_error()))
+        correct_for_merging(ctx, cols, merger, i)
+        runs.append(ops.run_from_columns(cols))
+    if len(runs) == 1:
+        return merger.getMergedHeader(), runs[0]
+    nb = [int(r.offsets[-1]) if r.n else 0 for r in runs]
+    keys = torch.cat([r.keys for r in runs])
+    vo = torch.cat([r.voffset for r in runs])
+    bs = torch.cat([r.block_size for r in runs])
+    pay = torch.cat([r.payload[:b] for r, b in zip(runs, nb)])
+    return merger.getMergedHeader(), ops.sort_received(keys, vo, bs, pay)

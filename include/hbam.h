@@ -200,16 +200,41 @@ int hbam_guess_batch(hbam_ctx* ctx, const uint8_t* file, int on_device, uint64_t
                      const int64_t* beg, const int64_t* end, uint64_t k, int32_t n_ref,
                      int64_t* out, int32_t* err);
 
-/* ---- BGZFSplitGuesser.guessNextBGZFBlockStart (util/BGZFSplitGuesser.java:51-92) --- */
+/* Windowed guesses: the bytes guessNextBAMRecordStart reads are the window
+ * file[beg, beg + min((int)(end-beg), 262139)) cut at the end of the file
+ * (BAMSplitGuesser.java:114-125; hbam_guess_window_len gives its length), so a client that
+ * does not hold the file (a JVM computing getSplits over HDFS) gathers those k windows and
+ * passes them concatenated: window i = windows[win_off[i], win_off[i+1]) (win_off: host,
+ * k+1 entries, win_off[0] = 0; a length other than hbam_guess_window_len -> HBAM_EINVAL).
+ * Same results as hbam_guess_batch over the whole file.  hbam_guess_batch itself stages only
+ * these windows when `file` is on the host. */
+uint64_t hbam_guess_window_len(uint64_t file_len, int64_t beg, int64_t end);
+int hbam_guess_windows(hbam_ctx* ctx, const uint8_t* windows, int on_device, const uint64_t* win_off,
+                       uint64_t file_len, const int64_t* beg, const int64_t* end, uint64_t k,
+                       int32_t n_ref, int64_t* out, int32_t* err);
+
+/* ---- BGZFSplitGuesser.guessNextBGZFBlockStart (util/BGZFSplitGuesser.java:51-92) ---
+ * The guesser reads one window of min((int)(end-beg), 131069) bytes at beg (:62-63):
+ * hbam_guess_bgzf_window takes that window alone (wlen = hbam_guess_bgzf_window_len). */
 int64_t hbam_guess_bgzf_block_start(hbam_ctx* ctx, const uint8_t* file, int on_device,
                                     uint64_t file_len, int64_t beg, int64_t end, int32_t* err);
+uint64_t hbam_guess_bgzf_window_len(uint64_t file_len, int64_t beg, int64_t end);
+int64_t hbam_guess_bgzf_window(hbam_ctx* ctx, const uint8_t* window, int on_device, uint64_t wlen,
+                               uint64_t file_len, int64_t beg, int64_t end, int32_t* err);
 
 /* ---- BAMInputFormat.getSplits for one file (BAMInputFormat.java:76-103,163-224):
  * Hadoop FileSplits [beg[i], end[i]) -> FileVirtualSplits.  Returns the number of
- * virtual splits, or a negative code ("no reads in first split" -> HBAM_EIO). */
+ * virtual splits, or a negative code ("no reads in first split" -> HBAM_EIO).
+ * hbam_probabilistic_splits_windows: the same from the file's first head_len bytes (host; the
+ * BAM header — HBAM_ETRUNC: too short, read more) and the guess windows of the n FileSplits
+ * (as hbam_guess_windows), for a client that reads only those bytes. */
 int64_t hbam_probabilistic_splits(hbam_ctx* ctx, const uint8_t* file, int on_device,
                                   uint64_t file_len, const uint64_t* beg, const uint64_t* end,
                                   uint64_t n, uint64_t* v_start, uint64_t* v_end);
+int64_t hbam_probabilistic_splits_windows(hbam_ctx* ctx, const uint8_t* head, uint64_t head_len,
+                                          const uint8_t* windows, int on_device, const uint64_t* win_off,
+                                          uint64_t file_len, const uint64_t* beg, const uint64_t* end,
+                                          uint64_t n, uint64_t* v_start, uint64_t* v_end);
 
 /* ---- Sort plugin path (Sort.java:84-188, SortReducer 191-205) ------
  * hbam_sort_keys: stable sort of n LongWritable keys (signed i64, Hadoop's comparator) on
@@ -255,6 +280,17 @@ int hbam_sort_split(hbam_ctx* ctx, const hbam_columns* dv, hbam_sorted_run* out)
  * rec_bounds / byte_bounds (host, nparts+1) get each partition's record and payload ranges. */
 int hbam_sort_partition(hbam_ctx* ctx, const hbam_sorted_run* run, const int64_t* split_points,
                         uint32_t nparts, uint64_t* rec_bounds, uint64_t* byte_bounds);
+/* Multi-input Sort (Sort.java:111-113 + SortRecordReader.nextKeyValue :279-295): when the inputs'
+ * sequence dictionaries differ, Utils.correctSAMRecordForMerging (cli/Utils.java:286-313) maps
+ * every record of input i onto the merged dictionary.  hbam_merge_remap does it on the device
+ * over a decoded split (dv, modified in place): refID -> ref_map[refID] (host, n_in entries =
+ * the input's dictionary size; -1 stays -1), next refID likewise for paired reads (flag 0x1),
+ * in the columns and in the record bytes, and the key recomputed (BAMRecordReader.getKey) where
+ * refID changed.  *bad_record = the first record whose new index lies outside its own input's
+ * dictionary (htsjdk resolves setReferenceIndex against the record's header: the reference
+ * throws IllegalArgumentException there), else UINT64_MAX.  Run it before hbam_sort_split. */
+int hbam_merge_remap(hbam_ctx* ctx, hbam_columns* dv, const int32_t* ref_map, int32_t n_in,
+                     uint64_t* bad_record);
 /* receive side: n records (device key/voffset/block_size and their packed payload, chunks in
  * source-rank order) as a sorted run */
 int hbam_sort_received(hbam_ctx* ctx, const int64_t* key, const int64_t* voffset,

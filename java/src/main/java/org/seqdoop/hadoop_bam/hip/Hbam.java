@@ -45,6 +45,17 @@ public final class Hbam implements AutoCloseable {
       FunctionDescriptor.of(J, A, A, I, J, J, J, I, A));
   static final MethodHandle SPLITS = fn("hbam_probabilistic_splits",
       FunctionDescriptor.of(J, A, A, I, J, A, A, J, A, A));
+  // split side over windows (a client never holds the file: HipBAMSplitGuesser,
+  // HipBAMInputFormat, HipBGZFSplitGuesser)
+  static final MethodHandle GUESS_WINDOW_LEN = fn("hbam_guess_window_len", FunctionDescriptor.of(J, J, J, J));
+  static final MethodHandle GUESS_WINDOWS = fn("hbam_guess_windows",
+      FunctionDescriptor.of(I, A, A, I, A, J, A, A, J, I, A, A));
+  static final MethodHandle GUESS_BGZF_WINDOW_LEN = fn("hbam_guess_bgzf_window_len",
+      FunctionDescriptor.of(J, J, J, J));
+  static final MethodHandle GUESS_BGZF_WINDOW = fn("hbam_guess_bgzf_window",
+      FunctionDescriptor.of(J, A, A, I, J, J, J, J, A));
+  static final MethodHandle SPLITS_WINDOWS = fn("hbam_probabilistic_splits_windows",
+      FunctionDescriptor.of(J, A, A, J, A, I, A, J, A, A, J, A, A));
   // SURVEY.md §8 f-4: Summarize ranges, FixMate shuffle + reducer, device -> host copies
   static final MethodHandle SUMMARIZE = fn("hbam_summarize_ranges", FunctionDescriptor.of(I, A, A, A));
   static final MethodHandle NAME_ORDER = fn("hbam_name_order", FunctionDescriptor.of(I, A, A, A, J, A));
@@ -116,6 +127,61 @@ public final class Hbam implements AutoCloseable {
   }
 
   public MemorySegment context() { return ctx; }
+
+  /** Bytes guessNextBAMRecordStart(beg, end) reads at beg (BAMSplitGuesser.java:114-125). */
+  public static long guessWindowLen(long fileLen, long beg, long end) {
+    try {
+      return (long) GUESS_WINDOW_LEN.invokeExact(fileLen, beg, end);
+    } catch (Throwable t) {
+      throw new RuntimeException(t);
+    }
+  }
+
+  /** Bytes guessNextBGZFBlockStart(beg, end) reads at beg (util/BGZFSplitGuesser.java:62-63). */
+  public static long guessBgzfWindowLen(long fileLen, long beg, long end) {
+    try {
+      return (long) GUESS_BGZF_WINDOW_LEN.invokeExact(fileLen, beg, end);
+    } catch (Throwable t) {
+      throw new RuntimeException(t);
+    }
+  }
+
+  /** Reads `len` bytes at `pos` the way BAMSplitGuesser buffers its window: read() calls until
+   *  `len` bytes or end of stream (:116-125). */
+  public static byte[] readWindow(htsjdk.samtools.seekablestream.SeekableStream in, long pos, int len)
+      throws IOException {
+    final byte[] b = new byte[len];
+    in.seek(pos);
+    int got = 0;
+    while (got < len) {
+      final int r = in.read(b, got, len - got);
+      if (r < 0) break;
+      got += r;
+    }
+    return got == len ? b : java.util.Arrays.copyOf(b, got);
+  }
+
+  /** hbam_guess_windows over k gathered windows (window i = windows[off[i], off[i+1])). */
+  public void guessWindows(byte[] windows, long[] off, long fileLen, long[] beg, long[] end, int nRef,
+                           long[] out, int[] err) throws IOException {
+    final int k = beg.length;
+    try (Arena a = Arena.ofConfined()) {
+      final MemorySegment w = a.allocate(Math.max(windows.length, 1));
+      MemorySegment.copy(windows, 0, w, ValueLayout.JAVA_BYTE, 0, windows.length);
+      final MemorySegment o = a.allocateFrom(J, off), b = a.allocateFrom(J, beg), e = a.allocateFrom(J, end);
+      final MemorySegment r = a.allocate(J, Math.max(k, 1)), er = a.allocate(I, Math.max(k, 1));
+      final int rc = (int) GUESS_WINDOWS.invokeExact(ctx, w, 0, o, fileLen, b, e, (long) k, nRef, r, er);
+      if (rc != OK) throw new IOException("hbam_guess_windows: " + lastError());
+      for (int i = 0; i < k; ++i) {
+        out[i] = r.getAtIndex(J, i);
+        err[i] = er.getAtIndex(I, i);
+      }
+    } catch (IOException | RuntimeException ex) {
+      throw ex;
+    } catch (Throwable t) {
+      throw new IOException(t);
+    }
+  }
 
   /** hbam_download: `bytes` of library-owned device memory into a new host segment of `arena`. */
   public MemorySegment download(MemorySegment dev, long bytes, Arena arena) {

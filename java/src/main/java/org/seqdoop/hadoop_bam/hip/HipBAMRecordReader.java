@@ -38,6 +38,19 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
   public static final String WINDOW_BYTES_PROPERTY = "hadoopbam.hip.window-bytes";
   public static final String DEVICE_PROPERTY = "hadoopbam.hip.device";
 
+  private static final ThreadLocal<Hbam> SPLIT_CTX = new ThreadLocal<Hbam>();
+
+  /** The split side's context: one per client thread (the guessers, like the reference's, are
+   *  not thread-safe), CRC checks on as in both guessers (BAMSplitGuesser.java:130). */
+  static Hbam context(Configuration conf) throws IOException {
+    Hbam h = SPLIT_CTX.get();
+    if (h == null) {
+      h = new Hbam(conf.getInt(DEVICE_PROPERTY, 0), true);
+      SPLIT_CTX.set(h);
+    }
+    return h;
+  }
+
   private final LongWritable key = new LongWritable();
   private final SAMRecordWritable record = new SAMRecordWritable();
   private boolean isInitialized = false;

@@ -54,6 +54,18 @@ static int64_t get_key0(int32_t ref, int32_t start0) {
   return (int64_t)((uint64_t)(int64_t)ref << 32) | (int64_t)start0;
 }
 
+/* Record layout bounds (a decoded split hands out records whose variable fields overrun
+ * block_size with status OK: htsjdk decodes those fields lazily and throws when one is read).
+ * cigar_ok: name + CIGAR inside the record (getCigar's read); layout_ok: every field. */
+static int cigar_ok(const uint8_t* r) {
+  const int64_t bs = rd32(r);
+  return bs >= 32 && 32 + (int64_t)R_LRN(r) + 4 * (int64_t)R_NCIG(r) <= bs;
+}
+static int layout_ok(const uint8_t* r) {
+  const int64_t bs = rd32(r), ls = R_LSEQ(r);
+  return bs >= 32 && ls >= 0 && 32 + (int64_t)R_LRN(r) + 4 * (int64_t)R_NCIG(r) + (ls + 1) / 2 + ls <= bs;
+}
+
 /* ---- Summarize (cli/plugins/chipster/Summarize.java:664-755) ---------------------------- */
 /* Java int arithmetic (wraps) */
 static int32_t iadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
@@ -63,7 +75,9 @@ static int32_t iadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint
  * the ranges delivered; *status = the exception nextKeyValue raises after them:
  *   OR_EREFID (IllegalArgumentException) — CigarOperator.binaryToEnum of an op code > 8;
  *   -13 (IndexOutOfBoundsException) — a record whose CIGAR yields no range: ranges.get(0)
- *   at :715.  cap too small -> -8. */
+ *   at :715;
+ *   OR_EFORMAT — the record's CIGAR lies outside its block_size (getCigar's lazy read throws
+ *   a runtime exception in htsjdk; its class is parity unpinned).  cap too small -> -8. */
 int64_t or_summarize_ranges(const uint8_t* pay, const uint64_t* off, uint64_t n, int32_t split_status,
                             int64_t* key, int32_t* beg, int32_t* end, uint8_t* rev, uint32_t* rec,
                             uint64_t cap, int32_t* status) {
@@ -76,6 +90,10 @@ int64_t or_summarize_ranges(const uint8_t* pay, const uint64_t* off, uint64_t n,
     const int32_t start = iadd(R_POS(r), 1); /* getAlignmentStart(), 1-based */
     /* :708-709 skip unmapped / unplaced records */
     if ((flag & 4u) || ref < 0 || start < 0) continue;
+    if (!cigar_ok(r)) {
+      *status = OR_EFORMAT;
+      return (int64_t)k;
+    }
     /* parseCIGAR (:719-755) */
     const uint8_t* cig = R_VAR(r) + R_LRN(r);
     const uint32_t nc = R_NCIG(r);
@@ -453,9 +471,17 @@ static int fm_emit(const fm_rec* f, uint32_t src, uint8_t* out_pay, uint64_t* ou
  * each a SAMRecordWritable payload at out_pay + out_off[k] and the input record it came from.
  * Reproduced quirk: when a primary is followed only by secondaries, the inner loop ends with b
  * = the last secondary, which is then mated and written a second time.  Returns the output
- * count; *status = OR_EFORMAT when a touched record's attributes do not parse. */
+ * count; *status = OR_EFORMAT when a touched record's attributes do not parse, or (no
+ * outputs) when any record's fields overrun its block_size: the mapper's getReadName / lazy
+ * field decode throws before the reducer runs. */
 int64_t or_fixmate(const uint8_t* pay, const uint64_t* off, uint64_t n, uint8_t* out_pay, uint64_t* out_off,
                    uint32_t* out_src, uint64_t cap, uint64_t pay_cap, int32_t* status) {
+  out_off[0] = 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (!layout_ok(pay + off[i])) {
+      *status = OR_EFORMAT;
+      return 0;
+    }
   uint32_t* perm = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
   if (!perm) return OR_ENOMEM;
   or_name_order(pay, off, n, perm);

@@ -292,6 +292,124 @@ def _regather(payload, offsets, order):
     return new_off, out
 
 
+# ---- multi-input Sort (Sort.java:111-113, 279-295; cli/Utils.java:252-325) -----------------
+def bam_dictionary(data):
+    """The sequence dictionary [(name, length)] of a BAM (zlib over the first members)."""
+    import struct
+    import zlib
+    d = bytes(np.asarray(data, np.uint8)[:64 << 20])
+    u, p = b"", 0
+    while p + 18 <= len(d):
+        bs = struct.unpack_from("<H", d, p + 16)[0] + 1
+        u += zlib.decompressobj(-15).decompress(d[p + 18:p + bs - 8])
+        p += bs
+        if len(u) >= 12:
+            lt = struct.unpack_from("<i", u, 4)[0]
+            q = 8 + lt
+            if len(u) >= q + 4:
+                n = struct.unpack_from("<i", u, q)[0]
+                q += 4
+                out, ok = [], True
+                for _ in range(n):
+                    if len(u) < q + 4:
+                        ok = False
+                        break
+                    ln = struct.unpack_from("<i", u, q)[0]
+                    if len(u) < q + 8 + ln:
+                        ok = False
+                        break
+                    out.append((u[q + 4:q + 3 + ln], struct.unpack_from("<i", u, q + 4 + ln)[0]))
+                    q += 8 + ln
+                if ok:
+                    return out
+    raise ValueError("truncated header")
+
+
+def merged_dictionary(dicts):
+    """SamFileHeaderMerger (htsjdk 1.131, mergeDictionaries = true; restated, parity unpinned):
+    -> (merged [(name, len)], merged?) — inputs folded left to right by mergeSequences."""
+    def same(a, b):
+        return len(a) == len(b) and all(x[0] == y[0] and (x[1] == y[1] or not x[1] or not y[1])
+                                        for x, y in zip(a, b))
+    if all(same(dicts[0], d) for d in dicts[1:]):
+        return list(dicts[0]), False
+    acc = []
+    for frm in dicts:
+        res = list(acc)
+        held = []
+        last = -1
+        for rec in frm:
+            at = next((k for k, r in enumerate(res) if r[0] == rec[0]), -1)
+            if at < 0:
+                held.append(rec)
+                continue
+            if at < last:
+                raise ValueError("sequence dictionaries in different orders")
+            res = res[:at] + held + res[at:]
+            last = at + len(held)
+            held = []
+        acc = res + held
+    return acc, True
+
+
+def correct_payloads(pay, off, keys, ref_map):
+    """Utils.correctSAMRecordForMerging + SortRecordReader's re-key on SAMRecordWritable
+    payloads (copy): refID -> ref_map, next refID too for paired reads, the coordinate key
+    recomputed where refID changed.  -> (payload, keys, first record raising or -1)."""
+    import struct
+    pay = np.array(pay, np.uint8, copy=True)
+    keys = np.array(keys, np.int64, copy=True)
+    n_in = len(ref_map)
+    for i in range(len(off) - 1):
+        o = int(off[i])
+        ref, pos = struct.unpack_from("<ii", pay, o + 4)
+        flag = struct.unpack_from("<H", pay, o + 18)[0]
+        mref = struct.unpack_from("<i", pay, o + 24)[0]
+
+        def tr(x):
+            return -1 if x == -1 else (int(ref_map[x]) if 0 <= x < n_in else n_in)
+        nr = tr(ref)
+        nm = tr(mref) if flag & 1 else mref
+        if nr >= n_in or nm >= n_in:
+            return pay, keys, i
+        if nr != ref:
+            struct.pack_into("<i", pay, o + 4, nr)
+            if not (flag & 4) and nr >= 0 and np.int32(pos + 1) >= 0:
+                keys[i] = (nr << 32) | pos  # getKey0: the int pos sign-extended before the OR
+        if nm != mref:
+            struct.pack_into("<i", pay, o + 24, nm)
+    return pay, keys, -1
+
+
+def sort_merged(datas):
+    """The multi-input Sort's total order over whole-file reads of every input: (key, input
+    index, voffset) -> (keys, payload, offsets, merged dictionary)."""
+    dicts = [bam_dictionary(d) for d in datas]
+    merged, did = merged_dictionary(dicts)
+    names = [n for n, _ in merged]
+    K, P, O, F, V = [], [], [], [], []
+    for fi, (d, dic) in enumerate(zip(datas, dicts)):
+        h = read_header(d)
+        cols = read_split(d, h["first_voffset"], (len(d) << 16) | 0xffff)
+        pay, off = record_payloads(cols)
+        keys = cols["key"].astype(np.int64)
+        if did:
+            pay, keys, bad = correct_payloads(pay, off, keys, [names.index(n) for n, _ in dic])
+            if bad >= 0:
+                raise ValueError("input %d record %d: index outside its dictionary" % (fi, bad))
+        for i in range(cols["n"]):
+            P.append(bytes(pay[int(off[i]):int(off[i + 1])]))
+        K.append(keys)
+        F.append(np.full(cols["n"], fi, np.int64))
+        V.append(cols["voffset"].astype(np.int64))
+    keys = np.concatenate(K)
+    o = np.lexsort((np.concatenate(V), np.concatenate(F), keys))
+    pays = [P[i] for i in o]
+    offs = np.zeros(len(o) + 1, np.int64)
+    offs[1:] = np.cumsum([len(x) for x in pays])
+    return keys[o], np.frombuffer(b"".join(pays), np.uint8), offs, merged
+
+
 # ---- read-name / CIGAR keyed consumers (SURVEY.md §8 f-4) ---------------------------------
 def _pay(payload, offsets):
     pay = np.ascontiguousarray(payload, np.uint8)

@@ -57,11 +57,26 @@ def summarize_edge_records():
     return R
 
 
+def overrun_record(field="cigar"):
+    """A mapped record whose n_cigar (field 'cigar') or l_seq ('seq') claims more bytes than its
+    block_size holds: decode hands it out with status OK and layout_ok 0, and htsjdk throws only
+    when the field is read (the consumers read such fields past the record)."""
+    b = bytearray(record(b"ovr", flag=0x41, ref=1, pos=60, cigar=((10, 0),), l_seq=10))
+    if field == "cigar":
+        struct.pack_into("<H", b, 16, 5000)     # n_cigar (payload offset 4 + 12)
+    else:
+        struct.pack_into("<i", b, 20, 1 << 20)  # l_seq (payload offset 4 + 16)
+    return bytes(b)
+
+
 def summarize_error_records(kind):
     """kind 'op': a CIGAR op code 9 in a mapped record (IllegalArgumentException); 'empty': a mapped
-    record whose CIGAR has no M/=/X (ranges.get(0) -> IndexOutOfBoundsException)."""
+    record whose CIGAR has no M/=/X (ranges.get(0) -> IndexOutOfBoundsException); 'overrun': a
+    mapped record whose CIGAR lies past its block_size (getCigar's read throws)."""
     R = summarize_edge_records()
-    if kind == "op":
+    if kind == "overrun":
+        R.insert(5, overrun_record("cigar"))
+    elif kind == "op":
         R.insert(5, record(b"x", flag=0, ref=1, pos=50, raw_ops=[(10 << 4) | 0, (3 << 4) | 9]))
     else:
         R.insert(5, record(b"x", flag=0, ref=1, pos=50, cigar=((5, 4), (3, 1)), l_seq=8))

@@ -50,3 +50,77 @@ def assert_same_split(got, ref, pools=True):
         assert np.array_equal(got["layout_ok"], op["layout_ok"])
         for k in ("names", "cigars", "seq", "qual", "aux"):
             assert np.array_equal(got[k], op[k]), "pool %s differs" % k
+
+
+def bgzf_pack(u, level=5, block=65280):
+    """BGZF members (zlib raw deflate) of the inflated stream u, plus the EOF block."""
+    import struct
+    import zlib
+    out = []
+    for p in range(0, len(u), block):
+        chunk = bytes(u[p:p + block])
+        co = zlib.compressobj(level, zlib.DEFLATED, -15)
+        cd = co.compress(chunk) + co.flush()
+        out.append(b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" +
+                   struct.pack("<H", len(cd) + 25) + cd + struct.pack("<II", zlib.crc32(chunk), len(chunk)))
+    out.append(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+    return b"".join(out)
+
+
+def bam_stream(data):
+    """inflated stream of a whole BAM (zlib)"""
+    import struct
+    import zlib
+    d = bytes(data)
+    u, p = [], 0
+    while p + 18 <= len(d):
+        bs = struct.unpack_from("<H", d, p + 16)[0] + 1
+        u.append(zlib.decompressobj(-15).decompress(d[p + 18:p + bs - 8]))
+        p += bs
+    return b"".join(u)
+
+
+def redictionary_bam(data, prepend=((b"chrNEW", 5000),), drop_last=1):
+    """A second input with a different dictionary, built from a BAM's records: `prepend` new
+    sequences, then the input's dictionary without its last `drop_last` sequences; every record
+    kept, its refIDs shifted up by len(prepend) (records on the dropped sequences left out).
+    Merged after the original (SamFileHeaderMerger.mergeSequences), the new sequences come first,
+    so the ORIGINAL's indices move up by len(prepend) — beyond its own dictionary when that
+    exceeds what it has after its records' sequences (the reference's IllegalArgumentException,
+    see hbam_merge_remap) — and this file's indices stay."""
+    import struct
+    u = bam_stream(data)
+    lt = struct.unpack_from("<i", u, 4)[0]
+    text = u[8:8 + lt]
+    p = 8 + lt
+    n = struct.unpack_from("<i", u, p)[0]
+    p += 4
+    refs = []
+    for _ in range(n):
+        ln = struct.unpack_from("<i", u, p)[0]
+        refs.append((u[p + 4:p + 3 + ln], struct.unpack_from("<i", u, p + 4 + ln)[0]))
+        p += 8 + ln
+    keep = len(refs) - drop_last
+    new_refs = list(prepend) + refs[:keep]
+    lines = [ln for ln in text.split(b"\n") if not ln.startswith(b"@SQ")]
+    sq = [b"@SQ\tSN:" + nm + b"\tLN:" + str(ln).encode() for nm, ln in new_refs]
+    hd = [ln for ln in lines if ln.startswith(b"@HD")]
+    rest = [ln for ln in lines if ln and not ln.startswith(b"@HD")]
+    new_text = b"\n".join(hd + sq + rest) + b"\n"
+    out = [b"BAM\x01", struct.pack("<i", len(new_text)), new_text, struct.pack("<i", len(new_refs))]
+    for nm, ln in new_refs:
+        out += [struct.pack("<i", len(nm) + 1), nm, b"\0", struct.pack("<i", ln)]
+    k = len(prepend)
+    while p + 4 <= len(u):
+        bs = struct.unpack_from("<i", u, p)[0]
+        r = bytearray(u[p:p + 4 + bs])
+        p += 4 + bs
+        ref, mref = struct.unpack_from("<i", r, 4)[0], struct.unpack_from("<i", r, 24)[0]
+        if ref >= keep or mref >= keep:
+            continue
+        if ref >= 0:
+            struct.pack_into("<i", r, 4, ref + k)
+        if mref >= 0:
+            struct.pack_into("<i", r, 24, mref + k)
+        out.append(bytes(r))
+    return np.frombuffer(bgzf_pack(b"".join(out)), np.uint8).copy(), refs, new_refs

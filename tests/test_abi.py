@@ -90,3 +90,48 @@ int main(void) {
     names = re.findall(r'withName\("(\w+)"\)', body)
     assert names == [f[0] for f in _lib.Columns._fields_]
     assert len(names) - 4 == 27
+
+
+_C2J = {"void": None}
+
+
+def _ctype_letter(t):
+    t = t.strip()
+    if "*" in t:
+        return "A"
+    t = t.replace("const", "").strip()
+    if t in ("int", "int32_t", "uint32_t"):
+        return "I"
+    if t in ("int64_t", "uint64_t", "size_t"):
+        return "J"
+    if t == "void":
+        return None
+    raise AssertionError("unmapped C type %r" % t)
+
+
+def _prototypes():
+    txt = open(os.path.join(ROOT, "include", "hbam.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    out = {}
+    for m in re.finditer(r"([A-Za-z_][\w ]*?\**)\s*\b(hbam_\w+)\s*\(([^)]*)\)\s*;", txt):
+        ret, name, params = m.group(1), m.group(2), m.group(3)
+        ps = [p for p in (x.strip() for x in params.split(",")) if p and p != "void"]
+        # a parameter's type: everything but its name
+        types = [re.sub(r"\b\w+$", "", p) if not p.endswith("*") else p for p in ps]
+        out[name] = (_ctype_letter(ret), [_ctype_letter(t) for t in types])
+    return out
+
+
+def test_java_downcalls_match_the_header():
+    """Every downcall the Java shim binds (Hbam.java fn(name, FunctionDescriptor...)) has the
+    header's return type and parameter list (A = pointer, I = 32-bit, J = 64-bit)."""
+    protos = _prototypes()
+    java = open(os.path.join(ROOT, "java", "src", "main", "java", "org", "seqdoop", "hadoop_bam",
+                             "hip", "Hbam.java")).read()
+    binds = re.findall(r'fn\("(hbam_\w+)",\s*FunctionDescriptor\.(of|ofVoid)\(([^)]*)\)\)', java)
+    assert len(binds) >= 20
+    for name, kind, args in binds:
+        assert name in protos, name
+        letters = [a.strip() for a in args.split(",") if a.strip()]
+        ret = None if kind == "ofVoid" else letters.pop(0)
+        assert (ret, letters) == protos[name], (name, (ret, letters), protos[name])

@@ -28,7 +28,8 @@ def _i64(x):
 def _fields(rec):
     import struct
     bs, ref, pos, lrn, mapq, bin_, nc, flag, lseq, nref, npos, tlen = struct.unpack_from("<iiiBBHHHiiii", rec)
-    cig = struct.unpack_from("<%dI" % nc, rec, 36 + lrn)
+    # a CIGAR past the record's block_size: getCigar's lazy read throws (None here)
+    cig = struct.unpack_from("<%dI" % nc, rec, 36 + lrn) if 32 + lrn + 4 * nc <= bs else None
     return dict(ref=ref, pos=pos, lrn=lrn, flag=flag, cigar=cig, name=bytes(rec[36:36 + max(lrn - 1, 0)]))
 
 
@@ -40,6 +41,8 @@ def py_summarize(recs):
         start = _i32(f["pos"] + 1)
         if (f["flag"] & 4) or f["ref"] < 0 or start < 0:
             continue
+        if f["cigar"] is None:
+            return out, -3
         ranges = []
         b = e = start
         for c in f["cigar"]:
@@ -87,7 +90,7 @@ def test_summarize_known_answer():
     assert list(r["key"]) == [(3 << 32) | 104, (3 << 32) | 114, (3 << 32) | 124, (3 << 32) | 133]
 
 
-@pytest.mark.parametrize("kind", [None, "op", "empty"])
+@pytest.mark.parametrize("kind", [None, "op", "empty", "overrun"])
 def test_summarize_oracle_vs_java_reading(kind):
     o = _oracle()
     recs = F.summarize_edge_records() if kind is None else F.summarize_error_records(kind)
@@ -225,7 +228,7 @@ def _same_ranges(got, want):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", [None, "op", "empty"])
+@pytest.mark.parametrize("kind", [None, "op", "empty", "overrun"])
 def test_summarize_device_edges(kind):
     recs = F.summarize_edge_records() if kind is None else F.summarize_error_records(kind)
     ctx = _ctx()
@@ -302,6 +305,23 @@ def test_fixmate_device_malformed_aux():
     pay, off = F.pack(recs)
     want = _oracle().fixmate(pay, off)
     assert want["status"] == -3
+    _same_fixmate(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("field", ["cigar", "seq"])
+def test_fixmate_device_layout_overrun(field):
+    """A record whose n_cigar / l_seq claims more bytes than its block_size holds (a decoded
+    split hands such a record out with status OK, layout_ok 0): the device never reads past the
+    record, and the job fails before any output as the oracle's (SAMFormatException)."""
+    recs = F.fixmate_records()[:40]
+    recs.insert(17, F.overrun_record(field))
+    ctx = _ctx()
+    tp, to, n = _dev_records(recs)
+    got = ctx.fixmate(tp.data_ptr(), to.data_ptr(), n)
+    pay, off = F.pack(recs)
+    want = _oracle().fixmate(pay, off)
+    assert want["status"] == -3 and len(want["src"]) == 0
     _same_fixmate(got, want)
 
 

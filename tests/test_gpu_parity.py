@@ -247,6 +247,120 @@ def test_guesses_window_exhaustion(gpu_ctx, oracle_mod, genbam, level, k):
         assert (int(out[i]), int(err[i])) == (g, e), i
 
 
+def _windows(ctx, data, beg, end, bgzf=False):
+    """The guess windows (the bytes each guess reads), concatenated, and their offsets."""
+    f = ctx.guess_bgzf_window_len if bgzf else ctx.guess_window_len
+    wl = [f(len(data), int(b), int(e)) for b, e in zip(beg, end)]
+    off = np.zeros(len(wl) + 1, np.uint64)
+    off[1:] = np.cumsum(wl)
+    parts = [data[int(b):int(b) + n] for b, n in zip(beg, wl) if n]
+    return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), off
+
+
+def _edge_offsets(n, rng, k):
+    beg = list(rng.integers(0, n, k)) + [0, 0, 1, n - 30, n - 2, n - 1, n, 5, 100, 4096]
+    end = [min(int(b) + int(rng.integers(1, 400000)), n) for b in beg[:k]] + \
+        [n, 3, 2, n, n, n, n, 5, 99, 4096 + 262139 + 7]
+    return np.array(beg, np.int64), np.array(end, np.int64)
+
+
+def test_guess_windows_match_oracle(gpu_ctx, oracle_mod):
+    """hbam_guess_windows over caller-gathered windows (host and device buffers) equals the
+    oracle's guess over the whole file, incl. windows cut by EOF, empty windows (end <= beg,
+    beg at EOF) and windows shorter than a BGZF header."""
+    import torch
+    data = _load("small_pe.bam")
+    h = oracle_mod.read_header(data)
+    beg, end = _edge_offsets(len(data), np.random.default_rng(13), 200)
+    w, off = _windows(gpu_ctx, data, beg, end)
+    assert int(off[-1]) < 200 * 262139 + 1
+    want = [oracle_mod.guess_bam_record_start(data, int(b), int(e), h["n_ref"]) for b, e in zip(beg, end)]
+    for src in (w, torch.from_numpy(w.copy()).cuda() if len(w) else w):
+        rc, out, err = gpu_ctx.guess_windows(src, off, len(data), beg, end, h["n_ref"])
+        assert rc == 0, gpu_ctx.last_error()
+        assert [(int(a), int(b)) for a, b in zip(out, err)] == [(int(g), int(e)) for g, e in want]
+    # the whole-file call from host memory stages only these windows and agrees
+    rc, out2, err2 = gpu_ctx.guess_batch(data, beg, end, h["n_ref"])
+    assert rc == 0 and np.array_equal(out2, out) and np.array_equal(err2, err)
+
+
+def test_guess_windows_reject_wrong_window(gpu_ctx, oracle_mod):
+    data = _load("small_pe.bam")
+    h = oracle_mod.read_header(data)
+    beg, end = np.array([1000, 90000], np.int64), np.array([500000, 95000], np.int64)
+    w, off = _windows(gpu_ctx, data, beg, end)
+    off[1] -= 1  # one byte short
+    rc, _, _ = gpu_ctx.guess_windows(w[:-1], off, len(data), beg, end, h["n_ref"])
+    assert rc == -11  # HBAM_EINVAL
+
+
+@pytest.mark.parametrize("name,split_size", [("small_pe.bam", 256 << 10), ("small_pe.bam", 64 << 10),
+                                             ("edge_uniform_long.bam", 128 << 10),
+                                             ("edge_htslib_empty.bam", 100 << 10)])
+def test_probabilistic_splits_windows(gpu_ctx, oracle_mod, name, split_size):
+    """getSplits from the header prefix + the FileSplits' guess windows only."""
+    data = _load(name)
+    b, e = oracle_mod.file_splits(len(data), split_size)
+    want = oracle_mod.probabilistic_splits(data, b, e)
+    w, off = _windows(gpu_ctx, data, b.astype(np.int64), e.astype(np.int64))
+    for hl in (1 << 20, 40):  # 40 bytes: too short for the header -> HBAM_ETRUNC
+        n, vs, ve = gpu_ctx.probabilistic_splits_windows(data[:hl], w, off, len(data), b, e)
+        if hl == 40:
+            assert n == -2
+            continue
+        if isinstance(want, int):
+            assert n == want
+            continue
+        assert n == len(want[0]) and np.array_equal(vs, want[0]) and np.array_equal(ve, want[1])
+
+
+def test_bgzf_guesser_window(gpu_ctx, oracle_mod):
+    data = _load("edge_uniform_long.bam")
+    rng = np.random.default_rng(4)
+    for beg in list(rng.integers(0, len(data) - 10, 30)) + [len(data) - 3, len(data)]:
+        end = min(int(beg) + int(rng.integers(10, 200000)), len(data))
+        wl = gpu_ctx.guess_bgzf_window_len(len(data), int(beg), end)
+        got = gpu_ctx.guess_bgzf_window(data[int(beg):int(beg) + wl], len(data), int(beg), end)
+        assert got == oracle_mod.guess_bgzf_block_start(data, int(beg), end)
+
+
+def test_mirror_guessers_read_only_windows(oracle_mod, tmp_path):
+    """The mirror's BAMSplitGuesser / getSplits read the header prefix and each guess window from
+    the file, never the whole file."""
+    from hadoop_bam import BAMInputFormat, BAMSplitGuesser, Configuration, compute_file_splits
+    data = _load("small_pe.bam")
+    big = tmp_path / "big.bam"
+    big.write_bytes(bytes(data))
+    reads = []
+
+    class Counting:
+        def __init__(self, f):
+            self.f = f
+
+        def seek(self, *a):
+            return self.f.seek(*a)
+
+        def read(self, n=-1):
+            b = self.f.read(n)
+            reads.append(len(b))
+            return b
+
+    with open(big, "rb") as f:
+        g = BAMSplitGuesser(Counting(f))
+        h = oracle_mod.read_header(data)
+        for beg in (0, 70000, 1 << 20, len(data) - 50000):
+            end = min(beg + (1 << 20), len(data))
+            assert g.guessNextBAMRecordStart(beg, end) == \
+                oracle_mod.guess_bam_record_start(data, beg, end, h["n_ref"])[0]
+    assert max(reads) <= max(262139, 1 << 20) and sum(reads) < len(data) * 2
+    fs = compute_file_splits(str(big), len(data), 256 << 10)
+    got = BAMInputFormat().getSplits(fs, Configuration())
+    b, e = oracle_mod.file_splits(len(data), 256 << 10)
+    vs, ve = oracle_mod.probabilistic_splits(data, b, e)
+    assert [(s.getStartVirtualOffset(), s.getEndVirtualOffset()) for s in got] == \
+        [(int(x), int(y)) for x, y in zip(vs, ve)]
+
+
 def test_bgzf_guesser(gpu_ctx, oracle_mod):
     data = _load("edge_uniform_long.bam")
     rng = np.random.default_rng(4)
@@ -311,7 +425,14 @@ def test_bad_refid_raises_illegal_argument_at_record(gpu_ctx, oracle_mod, genbam
 
 # ---- the drop-in API ---------------------------------------------------------------------
 def test_bam_input_format_record_reader(oracle_mod, tmp_path):
-    from hadoop_bam import BAMInputFormat, Configuration, compute_file_splits
+    """getSplits + createRecordReader + nextKeyValue through the mirror: every handed-out
+    (key, value) equals the oracle's BAMRecordReader over the same FileVirtualSplits — the key,
+    the value's wire bytes (SAMRecordWritable.write = BAMRecordCodec.encode of the untouched
+    record), every getter (fixed fields, name, CIGAR, SEQ, QUAL) against an independent host
+    decode of the oracle's record bytes, and the write/readFields round trip."""
+    import io
+    from hadoop_bam import BAMInputFormat, Configuration, SAMRecordWritable, compute_file_splits
+    from hadoop_bam.formats import BAMRecordBytes
     path = os.path.join(GOLDEN, "small_pe.bam")
     data = _load("small_pe.bam")
     fmt = BAMInputFormat()
@@ -324,17 +445,39 @@ def test_bam_input_format_record_reader(oracle_mod, tmp_path):
     for s in splits:
         owner = max(j for j, b in enumerate(starts) if b <= s.getStartVirtualOffset() >> 16)
         assert s.getLocations() == ["host%d" % owner]
-    keys = []
-    for s in splits:
-        rr = fmt.createRecordReader(s, Configuration())
-        while rr.nextKeyValue():
-            keys.append(rr.getCurrentKey().get())
-    want = []
     b, e = oracle_mod.file_splits(len(data), 512 << 10)
     vs, ve = oracle_mod.probabilistic_splits(data, b, e)
-    for a, z in zip(vs, ve):
-        want.extend(int(k) for k in oracle_mod.read_split(data, int(a), int(z), keep_var=False)["key"])
-    assert keys == want
+    assert [(s.getStartVirtualOffset(), s.getEndVirtualOffset()) for s in splits] == \
+        [(int(x), int(y)) for x, y in zip(vs, ve)]
+    getters = ("getReferenceIndex", "getAlignmentStart", "getFlags", "getReadUnmappedFlag",
+               "getMappingQuality", "getMateReferenceIndex", "getMateAlignmentStart",
+               "getInferredInsertSize", "getIndexingBin", "getReadName", "getCigarString",
+               "getReadString", "getBaseQualities", "getReadBases", "getVariableBinaryRepresentation")
+    n_total = 0
+    for s, a, z in zip(splits, vs, ve):
+        ref = oracle_mod.read_split(data, int(a), int(z))
+        pay, off = oracle_mod.record_payloads(ref)
+        rr = fmt.createRecordReader(s, Configuration())
+        k = 0
+        while rr.nextKeyValue():
+            assert rr.getCurrentKey().get() == int(ref["key"][k])
+            v = rr.getCurrentValue()
+            want_bytes = bytes(pay[int(off[k]):int(off[k + 1])])
+            rec = v.get()
+            assert rec.toBAMBytes() == want_bytes, k
+            want = BAMRecordBytes(want_bytes)
+            for g in getters:
+                assert getattr(rec, g)() == getattr(want, g)(), (k, g)
+            buf = io.BytesIO()
+            v.write(buf)
+            back = SAMRecordWritable()
+            back.readFields(io.BytesIO(buf.getvalue()))
+            assert back.get().toBAMBytes() == want_bytes
+            k += 1
+        assert k == ref["n"]
+        n_total += k
+        rr.close()
+    assert n_total > 10000
 
 
 # ---- full-size properties --------------------------------------------------------------

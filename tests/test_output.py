@@ -76,7 +76,22 @@ def _inputs():
         bs = struct.unpack_from("<H", data, p + 16)[0] + 1
         u += zlib.decompressobj(-15).decompress(data[p + 18:p + bs - 8])
         p += bs
+    # Fibonacci byte counts (1, 1, 2, 3, 5, ...) in random order: the Huffman tree of the
+    # literals is deeper than 15, so the lit/len code must be length-limited (an
+    # under-repaired limit left the code over-subscribed and zlib rejected the member)
+    fib = [1, 1]
+    while len(fib) < 22:
+        fib.append(fib[-1] + fib[-2])
+    fib_bytes = np.repeat(np.arange(22, dtype=np.uint8) * 11, fib)
+    rng.shuffle(fib_bytes)
+    # skewed random blocks: per block a Pareto-distributed byte histogram
+    skew = []
+    for _ in range(6):
+        w = rng.pareto(0.6, 256) + 1e-3
+        skew.append(rng.choice(256, 65280, p=w / w.sum()).astype(np.uint8))
     return {
+        "fib_literals": fib_bytes.tobytes(),
+        "skewed": np.concatenate(skew).tobytes(),
         "one": b"A",
         "small": bytes(range(256)) * 3,
         "block": rng.integers(0, 4, 65280, dtype=np.uint8).tobytes(),
