@@ -562,6 +562,33 @@ int hbam_upload(hbam_ctx* c, const uint8_t* host, uint64_t len, uint8_t** dev_ou
   return HBAM_OK;
 }
 
+// Page-lock a caller-owned host range for this library's HIP runtime (hipHostRegister).  The
+// streamed reader's host->device window copies are asynchronous only from page-locked memory;
+// memory another runtime pinned (PyTorch-ROCm ships its own libamdhip64) is pageable here.
+int hbam_host_register(hbam_ctx* c, void* host, uint64_t len) {
+  if (!c || (len && !host)) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!len) return HBAM_OK;
+  const hipError_t e = hipHostRegister(host, len, hipHostRegisterDefault);
+  if (e == hipErrorHostMemoryAlreadyRegistered) {
+    (void)hipGetLastError();
+    return HBAM_OK;
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(c, HBAM_EDEVICE, "hipHostRegister(%llu bytes): %s", (unsigned long long)len, hipGetErrorString(e));
+  }
+  return HBAM_OK;
+}
+
+int hbam_host_unregister(hbam_ctx* c, void* host) {
+  if (!c || !host) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  const hipError_t e = hipHostUnregister(host);
+  if (e != hipSuccess) (void)hipGetLastError();
+  return HBAM_OK;
+}
+
 int hbam_download(hbam_ctx* c, const void* dev, uint64_t bytes, void* host) {
   if (!c || (bytes && (!dev || !host))) return HBAM_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));

@@ -249,6 +249,9 @@ __device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64
     }
   }
 }
+#ifndef HBAM_RS_SERIAL
+#define HBAM_RS_SERIAL 1  // ordered matches: round 1 in parallel, the rest in order on one lane
+#endif
 #ifndef HBAM_RS_WAVES
 // waves per SIMD asked of the register allocator: 8 = the hardware maximum, which the 4.9 KiB of
 // LDS per block also allows (VGPRs 75 -> 64, 2 spilled): k_resolve 47.4 -> 42.6 ms at 10 GB
@@ -447,6 +450,61 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
         rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
         rs_bits(s_pend, p - s0, len, false);
       };
+#if HBAM_RS_SERIAL
+      // Round 1 on every lane: the matches whose source has no pending byte (60 % of the
+      // ordered ones on BAM data).  The rest then run in program order on one lane: a pending
+      // byte of a match's source is written by a match that starts before it, so in-order
+      // execution only ever reads final bytes.  The dataflow rounds this replaces took 4.4
+      // rounds per stretch (295 per block, each ~3.7 k cycles of LDS latency) for the ~13
+      // matches per stretch left after round 1 (tools/rounds_sim.py).
+      uint32_t ready = (live & 1u) && is_ready(rec0) ? 1u : 0u;
+#pragma unroll 1
+      for (uint32_t t = 1; t < mine; ++t)
+        if ((live >> t & 1u) && is_ready(rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos))) ready |= 1u << t;
+      rs_lds_order();
+      if (ready & 1u) {
+        const uint32_t p = (uint32_t)rec0 & 0xffffu, len = (uint32_t)(rec0 >> 16) & 0xffffu,
+                       dist = (uint32_t)(rec0 >> 32) & 0xffffu;
+        rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
+      }
+#pragma unroll 1
+      for (uint32_t t = 1; t < mine; ++t)
+        if (ready >> t & 1u) {
+          const uint64_t rec = rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos);
+          rs_copy_lds(s_buf, lbase + ((uint32_t)rec & 0xffffu), (uint32_t)(rec >> 16) & 0xffffu,
+                      (uint32_t)(rec >> 32) & 0xffffu, s_sel);
+        }
+      live &= ~ready;
+#ifdef HBAM_PROF
+      ++n_bat;
+#endif
+      if (__any(live != 0u)) {
+        // which ordered matches round 1 ran: bit j of s_pend[2t .. 2t+1] for match j = lane + 64t
+        // (the pending bitmap is not needed any more)
+        const uint32_t nslot = (nord + 63u) / 64u;
+#pragma unroll 1
+        for (uint32_t t = 0; t < nslot; ++t) {
+          const uint64_t m = __ballot(t < mine && (ready >> t & 1u));
+          if (lane == 0) {
+            s_pend[2 * t] = (uint32_t)m;
+            s_pend[2 * t + 1] = (uint32_t)(m >> 32);
+          }
+        }
+        rs_lds_order();
+        if (lane == 0) {
+#pragma unroll 1
+          for (uint32_t j = 0; j < nord; ++j) {
+            if (s_pend[j >> 5] >> (j & 31u) & 1u) continue;
+            const uint64_t rec = rs_unpack(s_rec[RS_MAXM - 1 - j], s_pos);
+            rs_copy_lds(s_buf, lbase + ((uint32_t)rec & 0xffffu), (uint32_t)(rec >> 16) & 0xffffu,
+                        (uint32_t)(rec >> 32) & 0xffffu, s_sel);
+          }
+        }
+#ifdef HBAM_PROF
+        ++n_bat;
+#endif
+      }
+#else
       for (;;) {
         uint32_t ready = (live & 1u) && is_ready(rec0) ? 1u : 0u;
 #pragma unroll 1
@@ -468,6 +526,7 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
         }
         rs_lds_order();
       }
+    #endif  // HBAM_RS_SERIAL
     }
 #else
     // ---- ordered matches: in-order batches

@@ -278,95 +278,6 @@ struct DirectSink {
   __device__ __forceinline__ void finish(uint32_t) {}
 };
 
-// TokenSink (phase 1 of the batched inflate): literals go to their final place in ubuf;
-// each match of >= 3 bytes leaves a 3-byte descriptor (len-3, dist-1 as u8 + u16 LE) in the
-// first bytes of its destination and a bit in the block's match-start bitmap; phase 2
-// (k_resolve) fills the holes.  Stores are 16-byte chunks (register write-combining) so the
-// lane never waits on its own byte stores; only the block's first/last chunk, which it
-// shares with the neighbouring blocks, is written bytewise.
-struct TokenSink {
-  uint8_t* ubuf;
-  uint64_t start;   // absolute output offset of the block
-  uint64_t end;     // start + isize
-  uint64_t cur;     // absolute 16-byte chunk held in lo/hi (~0 = none)
-  uint64_t lo, hi;
-  uint32_t* bm;     // match-start bitmap of the block (ceil(isize/32) words)
-  uint32_t bw, bword, nwords;
-  uint32_t* tail;   // [0] = op | n<<16 | 1<<31 for a final match shorter than 3 bytes, [1] = dist
-
-#ifdef HBAM_AB_NOSTORE
-  uint64_t ab_acc = 0;  // A/B build only: output stores replaced by a register fold
-#endif
-  __device__ __forceinline__ void flush() {
-    if (cur == ~0ULL) return;
-#ifdef HBAM_AB_NOSTORE
-    ab_acc ^= lo ^ (hi << 1) ^ cur;
-    return;
-#endif
-    if (cur >= start && cur + 16 <= end) {
-      uint4 v;
-      v.x = (uint32_t)lo; v.y = (uint32_t)(lo >> 32); v.z = (uint32_t)hi; v.w = (uint32_t)(hi >> 32);
-      st_out((uint4*)(ubuf + cur), v);
-    } else {
-      for (uint32_t k = 0; k < 16; ++k) {
-        const uint64_t a = cur + k;
-        if (a >= start && a < end) ubuf[a] = (uint8_t)((k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8))) & 0xff);
-      }
-    }
-  }
-  __device__ __forceinline__ void put(uint32_t op, uint32_t b) {
-    const uint64_t a = start + op;
-    const uint64_t c = a & ~15ULL;
-    if (c != cur) {
-      flush();
-      cur = c;
-      lo = 0;
-      hi = 0;
-    }
-    const uint32_t k = (uint32_t)(a & 15);
-    if (k < 8) lo |= (uint64_t)(b & 0xff) << (8 * k);
-    else hi |= (uint64_t)(b & 0xff) << (8 * (k - 8));
-  }
-  __device__ __forceinline__ void mark(uint32_t op) {
-    const uint32_t w = op >> 5;
-    while (bw < w) {
-#ifdef HBAM_AB_NOSTORE
-      ab_acc += bword;
-#else
-      st_out(bm + bw, bword);
-#endif
-      bword = 0;
-      ++bw;
-    }
-    bword |= 1u << (op & 31);
-  }
-  __device__ __forceinline__ void literal(uint32_t op, uint32_t b) { put(op, b); }
-  __device__ __forceinline__ void match(uint32_t op, uint32_t n, uint32_t dist) {
-    if (n >= 3) {
-      const uint32_t d = dist - 1;
-      put(op, n - 3);
-      put(op + 1, d & 0xff);
-      put(op + 2, d >> 8);
-      mark(op);
-    } else {
-      tail[0] = op | n << 16 | 0x80000000u;
-      tail[1] = dist;
-    }
-  }
-  __device__ __forceinline__ void finish(uint32_t) {
-    flush();
-#ifdef HBAM_AB_NOSTORE
-    if (end > start) ubuf[start] = (uint8_t)(ab_acc ^ (ab_acc >> 8) ^ (ab_acc >> 40));
-    return;
-#endif
-    while (bw < nwords) {
-      st_out(bm + bw, bword);
-      bword = 0;
-      ++bw;
-    }
-  }
-};
-
 // Inflate one raw DEFLATE stream (cdata, nbytes) to exactly isize bytes through `sink`.
 // syms_ll: 288 LDS slots, u16 (symbol) or u8 (symbol & 255; bit 8 from Huff.hlim, which halves
 // the batched inflate's LDS so two waves fit per SIMD); syms_d: 32 u8 LDS slots; lens: 352 B

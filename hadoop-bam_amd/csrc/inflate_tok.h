@@ -71,21 +71,24 @@ constexpr uint32_t TOK_K = HBAM_TOK_K;
 // three separate sink calls: 66.7 ms)
 #define HBAM_TOK_SPEC 1
 #endif
-#ifndef HBAM_TOK_MARK1
-#define HBAM_TOK_MARK1 0  // A/B: match-start bitmap window change as an if + rare zero loop
-#endif
-#ifndef HBAM_TOK_LIT3
-#define HBAM_TOK_LIT3 0  // A/B: up to three literals per fast-path iteration
-#endif
 // stream bits one fast-path iteration may consume: 2 lit/len codes + length extra + distance
-// code + distance extra = 15+15+5+15+13 = 63 (<= 64); with a third lit/len code 78 (<= 80)
-constexpr uint32_t TOK_FAST_BITS = HBAM_TOK_LIT3 ? 80u : 64u;
+// code + distance extra = 15+15+5+15+13 = 63 (<= 64)
+constexpr uint32_t TOK_FAST_BITS = 64u;
 constexpr uint32_t TOK_LENS_LL = 32;    // lens scratch: lit/len code lengths at +32 ..
 constexpr uint32_t TOK_LENS_D = 320;    //               distance code lengths at +320 (<= 30)
 
 // ---- input: two register banks + one quad in flight ------------------------------------
 typedef const __attribute__((address_space(1))) u32x4_t* gq_ptr;  // global (not flat) loads
-__device__ __forceinline__ u32x4_t ein_load(const uint4* p) { return *(gq_ptr)p; }
+#ifndef HBAM_TOK_NTLOAD
+#define HBAM_TOK_NTLOAD 0  // A/B: non-temporal compressed-input loads (L2 traffic of the pass)
+#endif
+__device__ __forceinline__ u32x4_t ein_load(const uint4* p) {
+#if HBAM_TOK_NTLOAD
+  return __builtin_nontemporal_load((gq_ptr)p);
+#else
+  return *(gq_ptr)p;
+#endif
+}
 struct EIn {
   const uint4* fp;    // quad held in t (merged at the next epoch); == fend when the fetch is done
   const uint4* fend;  // one past the last quad that holds stream bytes
@@ -305,9 +308,6 @@ struct TSink {
   uint32_t w0, w1, w2, w3;
   uint32_t* tail;   // [0] = op | n<<16 | 1<<31 for a final match shorter than 3 bytes, [1] = dist
   uint8_t* edge;    // 32 B: the block's partial first / last 16-byte chunk (k_edge_merge)
-#ifdef HBAM_AB_NOSTORE
-  uint64_t ab = 0;
-#endif
 
   __device__ __forceinline__ void init(uint8_t* ubuf, uint64_t start, uint32_t isize, uint32_t* bmp,
                                        uint32_t* tl, uint8_t* eg) {
@@ -327,10 +327,6 @@ struct TSink {
   __device__ __forceinline__ void flush() {
     if (curc == ~0u) return;
     const uint32_t r0 = curc << 4;
-#ifdef HBAM_AB_NOSTORE
-    ab ^= lo ^ (hi << 1) ^ r0;  // A/B build only: output stores replaced by a register fold
-    return;
-#endif
     // A chunk shared with a neighbouring block (the block's first chunk when it does not
     // start 16-aligned, its last when it does not end so) goes to the block's edge slot
     // instead, whole; k_edge_merge writes this block's bytes of it afterwards.  So every flush
@@ -348,29 +344,15 @@ struct TSink {
     }
   }
   __device__ __forceinline__ void win_store() {
-#ifdef HBAM_AB_NOSTORE
-    ab += w0 ^ w1 ^ w2 ^ w3;
-    return;
-#endif
     st_out((uint4*)(bm + 4u * bwin), make_uint4(w0, w1, w2, w3));
   }
   __device__ __forceinline__ void mark(uint32_t op) {
     const uint32_t w = op >> 7;
-#if HBAM_TOK_MARK1
-    // one window change per call in the common case; windows skipped by a long match or a
-    // literal run (no match start in them) are stored as zeros in a rarely taken loop
-    if (bwin < w) {
-      win_store();
-      w0 = w1 = w2 = w3 = 0;
-      for (++bwin; bwin < w; ++bwin) win_store();
-    }
-#else
     while (bwin < w) {
       win_store();
       w0 = w1 = w2 = w3 = 0;
       ++bwin;
     }
-#endif
     const uint32_t i = op & 127u, m = 1u << (i & 31u), q = i >> 5;
     w0 |= q == 0u ? m : 0u;
     w1 |= q == 1u ? m : 0u;
@@ -451,7 +433,7 @@ struct TSink {
     hi = sp ? 0ull : hi;
     if (em) mark(op);
   }
-  // One iteration's output as one packet: nb (<= 5, or 6 with HBAM_TOK_LIT3) bytes P (LSB first) at ubuf position
+  // One iteration's output as one packet: nb (<= 5) bytes P (LSB first) at ubuf position
   // soff + op: up to two literals and a 3-byte match descriptor, always contiguous, so one
   // chunk switch and at most one spill into the next chunk (tok_fast_spec).
   __device__ __forceinline__ void put(uint32_t op, uint64_t P, uint32_t nb) {
@@ -459,7 +441,7 @@ struct TSink {
     const uint32_t r = soff + op;
     const uint32_t c = r >> 4, k = r & 15u;
     switch_if(any && c != curc, c);
-    // shift amounts below 64 in every select arm (P < 2^48: at most 6 bytes)
+    // shift amounts below 64 in every select arm (P < 2^40: at most 5 bytes)
     const uint32_t kl = k < 8u ? k : 0u, kh = k < 8u ? 0u : k - 8u;
     const uint32_t kr = (k > 1u && k < 8u) ? 64u - 8u * k : 8u;
     lo |= k < 8u ? P << (8u * kl) : 0ull;
@@ -480,9 +462,6 @@ struct TSink {
       w0 = w1 = w2 = w3 = 0;
       ++bwin;
     }
-#ifdef HBAM_AB_NOSTORE
-    if (iend > soff) cbase[soff] = (uint8_t)(ab ^ (ab >> 13) ^ (ab >> 41));
-#endif
   }
 };
 
@@ -600,20 +579,7 @@ __device__ __forceinline__ uint32_t tok_fast(EIn& in, const HuffP& hl, const Huf
     if (sym < 256u) {
       if (op == isize) return 2u;
       sink.literal(op++, sym);
-#if HBAM_TOK_LIT3
-      // third lit/len code after two literals (the iteration's bit budget: TOK_FAST_BITS)
-      ein_refill(in);
-      if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) return 3u;
-      sym = (uint32_t)syms_ll[idx] | hi;
-      ein_drop(in, L);
-      if (sym < 256u) {
-        if (op == isize) return 2u;
-        sink.literal(op++, sym);
-        return 0u;
-      }
-#else
       return 0u;
-#endif
     }
   }
   if (sym == 256u) return 1u;
@@ -733,24 +699,8 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   ex = (ex == 0u && lit2 && op == isize) ? 2u : ex;
   const bool emit2 = ex == 0u && lit2;
   op += emit2 ? 1u : 0u;
-#if HBAM_TOK_LIT3
-  // a third lit/len code after two literals (bit budget TOK_FAST_BITS = 80: one refill here)
-  ein_refill(in);
-  uint32_t L3, idx3, hi3 = 0;
-  const bool ok3 = huffp_lookup<true>(hl, ein_rev15(in), L3, idx3, hi3);
-  const uint32_t sym3 = (uint32_t)syms_ll[ok3 ? idx3 : 0u] | hi3;
-  ex = (emit2 && !ok3) ? 3u : ex;
-  ein_drop(in, (emit2 && ok3) ? L3 : 0u);
-  const bool lit3 = emit2 && ok3 && sym3 < 256u;
-  ex = (ex == 0u && lit3 && op == isize) ? 2u : ex;
-  const bool emit3 = ex == 0u && lit3;
-  op += emit3 ? 1u : 0u;
-  const uint32_t m = emit2 ? sym3 : emit1 ? sym2 : sym1;
-  const bool ism = ex == 0u && (emit2 ? !lit3 : emit1 ? !lit2 : !lit1);
-#else
   const uint32_t m = emit1 ? sym2 : sym1;
   const bool ism = ex == 0u && !emit2 && !lit2;
-#endif
   ex = (ism && m == 256u) ? 1u : ex;
   ex = (ism && m > 285u) ? 3u : ex;
   const bool dom = ism && m > 256u && m <= 285u;
@@ -784,12 +734,7 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   const bool em = domatch && n >= 3u;
   uint64_t P = emit1 ? (uint64_t)(sym1 & 0xffu) : 0ull;
   P |= emit2 ? (uint64_t)(sym2 & 0xffu) << 8 : 0ull;
-#if HBAM_TOK_LIT3
-  P |= emit3 ? (uint64_t)(sym3 & 0xffu) << 16 : 0ull;
-  const uint32_t nl = (emit1 ? 1u : 0u) + (emit2 ? 1u : 0u) + (emit3 ? 1u : 0u);
-#else
   const uint32_t nl = (emit1 ? 1u : 0u) + (emit2 ? 1u : 0u);
-#endif
   P |= em ? (uint64_t)((n - 3u) | (dist - 1u) << 8) << (8u * nl) : 0ull;
   sink.put(op1, P, nl + (em ? 3u : 0u));
   if (em) sink.mark(op);

@@ -51,6 +51,7 @@ EXPORTS = [
     "hbam_summarize_ranges", "hbam_name_order", "hbam_fixmate", "hbam_download",
     "hbam_guess_window_len", "hbam_guess_windows", "hbam_guess_bgzf_window_len",
     "hbam_guess_bgzf_window", "hbam_probabilistic_splits_windows", "hbam_merge_remap",
+    "hbam_host_register", "hbam_host_unregister",
 ]
 
 
@@ -193,6 +194,8 @@ def load(path=None):
         "hbam_sort_partition": (C.c_int, [vp, C.POINTER(SortedRunC), vp, C.c_uint32, vp, vp]),
         "hbam_sort_received": (C.c_int, [vp, vp, vp, vp, vp, C.c_uint64, C.POINTER(SortedRunC)]),
         "hbam_merge_remap": (C.c_int, [vp, C.POINTER(Columns), vp, C.c_int32, C.POINTER(C.c_uint64)]),
+        "hbam_host_register": (C.c_int, [vp, vp, C.c_uint64]),
+        "hbam_host_unregister": (C.c_int, [vp, vp]),
         "hbam_bgzf_bound": (C.c_uint64, [C.c_uint64, C.c_uint32]),
         "hbam_summarize_ranges": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(RangesC)]),
         "hbam_name_order": (C.c_int, [vp, vp, vp, C.c_uint64, vp]),

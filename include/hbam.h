@@ -135,6 +135,11 @@ int hbam_get_timing(const hbam_ctx* ctx, hbam_timing* out);
 /* ---- device staging (the Java shim maps HDFS bytes into pinned buffers) ---------- */
 int hbam_upload(hbam_ctx* ctx, const uint8_t* host, uint64_t len, uint8_t** dev_out);
 int hbam_device_free(hbam_ctx* ctx, uint8_t* dev);
+/* page-lock / release a caller-owned host range (hipHostRegister) so hbam_split_next's window
+ * copies run asynchronously beside the decode; memory pinned by another HIP runtime in the
+ * process (PyTorch-ROCm's) is pageable to this library */
+int hbam_host_register(hbam_ctx* ctx, void* host, uint64_t len);
+int hbam_host_unregister(hbam_ctx* ctx, void* host);
 /* copy `bytes` of library-owned device memory (e.g. an f-4 output) to host memory, ordered after
  * the context's work */
 int hbam_download(hbam_ctx* ctx, const void* dev, uint64_t bytes, void* host);

@@ -40,6 +40,8 @@ public final class Hbam implements AutoCloseable {
   static final MethodHandle SPLIT_OPEN = fn("hbam_split_open",
       FunctionDescriptor.of(A, A, A, J, J, J, I, J));
   static final MethodHandle SPLIT_NEXT = fn("hbam_split_next", FunctionDescriptor.of(I, A, A));
+  static final MethodHandle HOST_REGISTER = fn("hbam_host_register", FunctionDescriptor.of(I, A, A, J));
+  static final MethodHandle HOST_UNREGISTER = fn("hbam_host_unregister", FunctionDescriptor.of(I, A, A));
   static final MethodHandle SPLIT_CLOSE = fn("hbam_split_close", FunctionDescriptor.ofVoid(A));
   static final MethodHandle GUESS = fn("hbam_guess_bam_record_start",
       FunctionDescriptor.of(J, A, A, I, J, J, J, I, A));
@@ -54,6 +56,13 @@ public final class Hbam implements AutoCloseable {
       FunctionDescriptor.of(J, J, J, J));
   static final MethodHandle GUESS_BGZF_WINDOW = fn("hbam_guess_bgzf_window",
       FunctionDescriptor.of(J, A, A, I, J, J, J, J, A));
+  // Sort plugin path (HipSort, HipSortRecordReader)
+  static final MethodHandle DEVICE_ALLOC = fn("hbam_device_alloc", FunctionDescriptor.of(I, A, J, A));
+  static final MethodHandle DEVICE_FREE = fn("hbam_device_free", FunctionDescriptor.of(I, A, A));
+  static final MethodHandle SORT_SPLIT = fn("hbam_sort_split", FunctionDescriptor.of(I, A, A, A));
+  static final MethodHandle SORT_PARTITION = fn("hbam_sort_partition", FunctionDescriptor.of(I, A, A, A, I, A, A));
+  static final MethodHandle SORT_RECEIVED = fn("hbam_sort_received", FunctionDescriptor.of(I, A, A, A, A, A, J, A));
+  static final MethodHandle MERGE_REMAP = fn("hbam_merge_remap", FunctionDescriptor.of(I, A, A, A, I, A));
   static final MethodHandle SPLITS_WINDOWS = fn("hbam_probabilistic_splits_windows",
       FunctionDescriptor.of(J, A, A, J, A, I, A, J, A, A, J, A, A));
   // SURVEY.md §8 f-4: Summarize ranges, FixMate shuffle + reducer, device -> host copies

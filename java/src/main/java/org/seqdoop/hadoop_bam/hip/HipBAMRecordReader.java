@@ -66,6 +66,15 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
   private BAMRecordCodec codec;
   private ValidationStringency stringency;
   private long fileStart, virtualEnd;
+  private int[] mergeMap;
+  private MemorySegment registered;  // the file bytes hbam_host_register locked  // HipSortRecordReader: merged index of each input index, or null
+
+  /** Utils.correctSAMRecordForMerging on the device for every window (hbam_merge_remap):
+   *  SortRecordReader (Sort.java:279-295) sets it when the inputs' dictionaries differ. */
+  void setMergeMap(int[] map) { mergeMap = map; }
+
+  SAMFileHeader header() { return codecHeader; }
+  private SAMFileHeader codecHeader;
 
   @Override public void initialize(InputSplit spl, TaskAttemptContext ctx) throws IOException {
     if (isInitialized) close();  // re-entrant, as the reference (:116-118)
@@ -82,12 +91,20 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     }
     // the lazy record of each hand-out is built from the record's bytes by htsjdk's own codec
     codec = new BAMRecordCodec(header);
+    codecHeader = header;
     final int nRef = header.getSequenceDictionary().size();
     final long len = fs.getFileStatus(file).getLen();
 
     arena = Arena.ofShared();
     final MemorySegment bytes = mapFile(fs, file, len, arena);
     hbam = new Hbam(conf.getInt(DEVICE_PROPERTY, 0), false);
+    // page-locked for the library's HIP runtime, so each window's copy overlaps the previous
+    // window's decode; a mapping the driver refuses to lock is still read (synchronously)
+    try {
+      registered = (int) Hbam.HOST_REGISTER.invokeExact(hbam.context(), bytes, len) == Hbam.OK ? bytes : null;
+    } catch (Throwable t) {
+      registered = null;
+    }
     fileStart = split.getStartVirtualOffset() >>> 16;
     virtualEnd = split.getEndVirtualOffset();
     try {
@@ -134,11 +151,21 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
 
   /** The next window's records (hbam_split_next + hbam_columns_to_host); false at the end. */
   private boolean nextWindow() {
+    long bad = -1;  // first record hbam_merge_remap refuses (HipSortRecordReader only)
     try {
       if (hostLive) { Hbam.FREE_HOST.invokeExact(host); hostLive = false; }
       final int rc = (int) Hbam.SPLIT_NEXT.invokeExact(stream, dev);
       if (rc < 0) throw new RuntimeIOException("hbam_split_next: " + hbam.lastError());
       if (rc == 0) { last = true; n = i = 0; return false; }
+      if (mergeMap != null) {
+        try (Arena a = Arena.ofConfined()) {
+          final MemorySegment m = a.allocateFrom(ValueLayout.JAVA_INT, mergeMap);
+          final MemorySegment b = a.allocate(ValueLayout.JAVA_LONG);
+          final int rc3 = (int) Hbam.MERGE_REMAP.invokeExact(hbam.context(), dev, m, mergeMap.length, b);
+          if (rc3 != Hbam.OK) throw new RuntimeIOException("hbam_merge_remap: " + hbam.lastError());
+          bad = b.get(ValueLayout.JAVA_LONG, 0);
+        }
+      }
       final int rc2 = (int) Hbam.COLUMNS_TO_HOST.invokeExact(hbam.context(), dev, host);
       if (rc2 != Hbam.OK) throw new RuntimeIOException("hbam_columns_to_host: " + hbam.lastError());
       hostLive = true;
@@ -150,6 +177,12 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     n = host.get(ValueLayout.JAVA_LONG, Hbam.offsetOf("n_records"));
     status = host.get(ValueLayout.JAVA_INT, Hbam.offsetOf("status"));
     if (status != Hbam.OK) last = true;
+    if (mergeMap != null && bad >= 0 && bad < n) {
+      // SAMRecord.setReferenceIndex against the record's own header throws here (:286-313)
+      n = bad;
+      status = Hbam.EREFID;
+      last = true;
+    }
     i = 0;
     keys = ptr(host, "key", 8 * n);
     voffs = ptr(host, "voffset", 8 * n);
@@ -194,11 +227,13 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     try {
       if (hostLive) Hbam.FREE_HOST.invokeExact(host);
       if (stream != null && stream.address() != 0) Hbam.SPLIT_CLOSE.invokeExact(stream);
+      if (registered != null) { final int rc = (int) Hbam.HOST_UNREGISTER.invokeExact(hbam.context(), registered); }
     } catch (Throwable t) {
       throw new IOException(t);
     } finally {
       hostLive = false;
       stream = null;
+      registered = null;
       if (hbam != null) hbam.close();
       hbam = null;
       if (arena != null) arena.close();

@@ -1,7 +1,10 @@
 """N>1 path on CPU: two gloo ranks shard one BAM file's FileSplits, all-gather their guesses
 and reproduce BAMInputFormat.addProbabilisticSplits exactly (incl. empty-split merges across
 the rank boundary).  The guesser/decoder stand-in here is the CPU oracle (test code only);
-on the GPU box the same module runs with the device guesser (tests/test_gpu_distributed.py)."""
+on the GPU box the sharded decode runs with the device guesser in
+tests/test_gpu_parity.py::test_sharded_split_windows_match_oracle, the two-process device Sort in
+tests/test_sort.py::test_two_process_gpu_sort_matches_total_order, and bench.py --gpus 2 in
+tests/test_bench.py."""
 import os
 import socket
 import sys
