@@ -22,6 +22,7 @@
 #include "hbam_internal.h"
 #include "hbam_kernels.hip"
 #include "hbam_guess.hip"
+#include "hbam_bcf.hip"
 #include "hbam_sort.hip"
 #include "hbam_deflate.hip"
 
@@ -156,6 +157,9 @@ enum BufId {
   B_F4_LENS,
   B_F4_OOFF,
   B_F4_PAY,
+  // BCF read path (hbam_bcf_api.hip)
+  B_BCF_COLS,
+  B_BCF_SCRATCH,
   B_COUNT_ALL
 };
 
@@ -1004,10 +1008,10 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if ((rc = ensure(c, B_RECBASE, wb + 1, &rbase))) return rc;
   if ((rc = ensure(c, B_BADLIST, wb + 1, &badlist))) return rc;
   if (wb > 1)
-    k_block_entry<<<(uint32_t)(wb - 1), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, n_ref,
+    k_block_entry<<<(uint32_t)(wb - 1), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, BamFmt{n_ref},
                                                             entry);
-  k_block_walk<<<grid_for(wb, 64), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, r0, hard_end, entry, rel,
-                                                       count, exitp);
+  k_block_walk<<<grid_for(wb, 64), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, r0, hard_end, BamFmt{n_ref},
+                                                       entry, rel, count, exitp);
   uint32_t* nbad_d = (uint32_t*)(small + 5);
   uint8_t* mark;
   if ((rc = ensure(c, B_MARK, wb + 1, &mark))) return rc;
@@ -1020,8 +1024,8 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   HIPCHK(c, hipMemcpyAsync(&nbad, nbad_d, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (nbad) {  // runs of mismatched blocks repaired in parallel, then whatever is left, in order
-    k_chain_fix_par<<<grid_for(nbad, 64), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, entry, rel,
-                                                               count, exitp, badlist, nbad, mark);
+    k_chain_fix_par<<<grid_for(nbad, 64), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, BamFmt{n_ref},
+                                                               entry, rel, count, exitp, badlist, nbad, mark);
     HIPCHK(c, hipMemsetAsync(nbad_d, 0, 4, c->stream));
     k_stitch_check<<<grid_for(wb - 1, 256), 256, 0, c->stream>>>(entry, exitp, (uint32_t)wb, nbad_d,
                                                                  badlist, (uint32_t)wb, nullptr);
@@ -1034,8 +1038,8 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
     HIPCHK(c, copy_sync(c, bl.data(), badlist, nbad * 4, hipMemcpyDeviceToHost));
     std::sort(bl.begin(), bl.end());
     HIPCHK(c, copy_sync(c, badlist, bl.data(), nbad * 4, hipMemcpyHostToDevice));
-    k_chain_fix<<<1, 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, entry, rel, count, exitp,
-                                         badlist, nbad);
+    k_chain_fix<<<1, 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, BamFmt{n_ref}, entry, rel, count,
+                                         exitp, badlist, nbad);
     HIPCHK(c, hipGetLastError());
   }
   uint64_t nrec = 0;
@@ -2222,3 +2226,4 @@ extern "C" int64_t hbam_bgzf_compress(hbam_ctx* c, const uint8_t* src, int src_o
 }
 
 #include "hbam_consumers.hip"
+#include "hbam_bcf_api.hip"

@@ -11,7 +11,7 @@ constexpr uint32_t SCAN_CAP = 64;       // candidate slots per chunk
 constexpr uint32_t INFLATE_WG = 64;     // lanes (= blocks) per inflate workgroup
 constexpr uint32_t LENS_SLOT = 352;     // per-block global scratch for code lengths
 constexpr uint32_t BITMAP_WORDS = 2048;  // per-block match-start bitmap (65536 bits)
-constexpr uint32_t WALK_CAP = 1824;     // >= 65536/36 record starts per block
+constexpr uint32_t WALK_CAP = 1880;     // >= 65536/35 record starts per block (BAM >= 36 B, BCF >= 35 B)
 constexpr uint32_t SCAN_WG = 256;
 constexpr uint64_t UBUF_SLACK = 8192;  // k_resolve reads whole 2 KiB stretches past a block end
 constexpr uint32_t SCAN_TILE = 4096;

@@ -25,12 +25,13 @@
 
 namespace hbam {
 
-static __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) {
-  return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
-}
-static __device__ __forceinline__ uint16_t ld_u16_unaligned(const uint8_t* p) {
-  return (uint16_t)(p[0] | p[1] << 8);
-}
+// Byte-aligned scalar fields as one global load each: the device runs in unaligned access mode
+// (as the LZ77 pass's 8-byte source loads rely on), so a 1-aligned u32 type compiles to a single
+// global_load_dword instead of four byte loads and three shifts.
+typedef uint32_t u32_a1 __attribute__((aligned(1)));
+typedef uint16_t u16_a1 __attribute__((aligned(1)));
+static __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) { return *(const u32_a1*)p; }
+static __device__ __forceinline__ uint16_t ld_u16_unaligned(const uint8_t* p) { return *(const u16_a1*)p; }
 
 // ------------------------------------------------------------------------------------
 // K1: candidate BGZF block starts.  htsjdk accepts a block when bytes 0..3 = 1f 8b 08 04
@@ -681,9 +682,26 @@ static __device__ __forceinline__ bool rec_plausible(const uint8_t* __restrict__
   return p[36 + L - 1] == 0;
 }
 
+// The chain walk is generic over the record format: Fmt::plausible(u, x, hard_end) is the
+// per-block entry predicate, Fmt::next(u, r, hard_end) the chain step from a record start
+// (CHAIN_STOP where the record cannot be framed: the decode reports it).
+struct BamFmt {  // BAMRecordCodec framing: r + 4 + block_size, block_size >= 32
+  int32_t n_ref;
+  __device__ __forceinline__ bool plausible(const uint8_t* __restrict__ u, uint64_t x, uint64_t hard_end) const {
+    return rec_plausible(u, x, hard_end, n_ref);
+  }
+  __device__ __forceinline__ uint64_t next(const uint8_t* __restrict__ u, uint64_t r, uint64_t hard_end) const {
+    if (r + 4 > hard_end) return CHAIN_STOP;
+    const int32_t bs = (int32_t)ld_u32_unaligned(u + r);
+    if (bs < 32) return CHAIN_STOP;
+    return r + 4 + (uint64_t)(uint32_t)bs;
+  }
+};
+
+template <typename Fmt>
 __global__ __launch_bounds__(64) void k_block_entry(const uint8_t* __restrict__ u,
                                                     const uint64_t* __restrict__ uoff, uint32_t nblk,
-                                                    uint64_t hard_end, int32_t n_ref,
+                                                    uint64_t hard_end, Fmt fmt,
                                                     uint64_t* __restrict__ entry) {
   const uint32_t b = blockIdx.x + 1;  // block 0's entry is the split start
   if (b >= nblk) return;
@@ -692,7 +710,7 @@ __global__ __launch_bounds__(64) void k_block_entry(const uint8_t* __restrict__ 
   uint64_t found = NO_ENTRY;
   for (uint64_t x0 = b0; x0 < b1 && found == NO_ENTRY; x0 += 64) {
     const uint64_t x = x0 + lane;
-    const bool c = (x < b1) && rec_plausible(u, x, hard_end, n_ref);
+    const bool c = (x < b1) && fmt.plausible(u, x, hard_end);
     uint64_t mask = __ballot(c);
     while (mask) {
       const int l = __ffsll((unsigned long long)mask) - 1;
@@ -703,10 +721,9 @@ __global__ __launch_bounds__(64) void k_block_entry(const uint8_t* __restrict__ 
       if (lane == 0) {
         uint64_t r = xc;
         for (int h = 0; h < 3 && ok; ++h) {
-          const int32_t bs = (int32_t)ld_u32_unaligned(u + r);
-          r += 4 + (uint64_t)(uint32_t)bs;
+          r = fmt.next(u, r, hard_end);
           if (r == hard_end) break;
-          ok = rec_plausible(u, r, hard_end, n_ref);
+          ok = r != CHAIN_STOP && fmt.plausible(u, r, hard_end);
         }
       }
       ok = __shfl(ok, 0);
@@ -718,9 +735,10 @@ __global__ __launch_bounds__(64) void k_block_entry(const uint8_t* __restrict__ 
 
 // Walk block b from entry[b]: record starts in [uoff[b], uoff[b+1]) are stored as u16
 // offsets (cap WALK_CAP per block); exit[b] = first chain position >= uoff[b+1], or
-// CHAIN_STOP when a record's block_size cannot be read / is < 32 (chain ends there).
+// CHAIN_STOP when a record cannot be framed (the chain ends there).
+template <typename Fmt>
 static __device__ void walk_one(const uint8_t* __restrict__ u, const uint64_t* __restrict__ uoff,
-                                uint32_t b, uint64_t r, uint64_t hard_end,
+                                uint32_t b, uint64_t r, uint64_t hard_end, const Fmt& fmt,
                                 uint16_t* __restrict__ rel, uint32_t* __restrict__ count,
                                 uint64_t* __restrict__ exitp) {
   const uint64_t b0 = uoff[b], b1 = uoff[b + 1];
@@ -738,23 +756,22 @@ static __device__ void walk_one(const uint8_t* __restrict__ u, const uint64_t* _
   while (r < b1) {
     if (n < WALK_CAP) rel[(uint64_t)b * WALK_CAP + n] = (uint16_t)(r - b0);
     ++n;
-    if (r + 4 > hard_end) { r = CHAIN_STOP; break; }
-    const int32_t bs = (int32_t)ld_u32_unaligned(u + r);
-    if (bs < 32) { r = CHAIN_STOP; break; }
-    r += 4 + (uint64_t)(uint32_t)bs;
+    r = fmt.next(u, r, hard_end);
+    if (r == CHAIN_STOP) break;
   }
   count[b] = n;
   exitp[b] = r;
 }
 
+template <typename Fmt>
 __global__ void k_block_walk(const uint8_t* __restrict__ u, const uint64_t* __restrict__ uoff,
-                             uint32_t nblk, uint64_t r0, uint64_t hard_end,
+                             uint32_t nblk, uint64_t r0, uint64_t hard_end, Fmt fmt,
                              const uint64_t* __restrict__ entry, uint16_t* __restrict__ rel,
                              uint32_t* __restrict__ count, uint64_t* __restrict__ exitp) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nblk) return;
   const uint64_t r = (b == 0) ? r0 : entry[b];
-  walk_one(u, uoff, b, r, hard_end, rel, count, exitp);
+  walk_one(u, uoff, b, r, hard_end, fmt, rel, count, exitp);
 }
 
 // mismatch list: blocks whose entry != predecessor's exit (mark: 1 per listed block, optional)
@@ -777,8 +794,9 @@ __global__ void k_stitch_check(const uint64_t* __restrict__ entry, const uint64_
 // lane), so no two lanes write one block.  A head whose predecessor another lane re-walked may
 // start from a stale exit: the stitch check after this pass catches that, and k_chain_fix
 // finishes in order.
+template <typename Fmt>
 __global__ void k_chain_fix_par(const uint8_t* __restrict__ u, const uint64_t* __restrict__ uoff,
-                                uint32_t nblk, uint64_t hard_end, uint64_t* __restrict__ entry,
+                                uint32_t nblk, uint64_t hard_end, Fmt fmt, uint64_t* __restrict__ entry,
                                 uint16_t* __restrict__ rel, uint32_t* __restrict__ count,
                                 uint64_t* __restrict__ exitp, const uint32_t* __restrict__ bad_list,
                                 uint32_t nbad, const uint8_t* __restrict__ mark) {
@@ -789,7 +807,7 @@ __global__ void k_chain_fix_par(const uint8_t* __restrict__ u, const uint64_t* _
   for (;;) {
     const uint64_t e = exitp[b - 1];
     entry[b] = e;
-    walk_one(u, uoff, b, e, hard_end, rel, count, exitp);
+    walk_one(u, uoff, b, e, hard_end, fmt, rel, count, exitp);
     ++b;
     if (b >= nblk || (mark[b] && !mark[b - 1])) break;  // the end, or the next run's head
     if (entry[b] == exitp[b - 1]) break;                 // consistent again
@@ -798,8 +816,9 @@ __global__ void k_chain_fix_par(const uint8_t* __restrict__ u, const uint64_t* _
 
 // Sequential repair (one lane): process mismatched blocks in order, re-walking from the
 // predecessor's exit and propagating until consistent again.
+template <typename Fmt>
 __global__ void k_chain_fix(const uint8_t* __restrict__ u, const uint64_t* __restrict__ uoff,
-                            uint32_t nblk, uint64_t hard_end, uint64_t* __restrict__ entry,
+                            uint32_t nblk, uint64_t hard_end, Fmt fmt, uint64_t* __restrict__ entry,
                             uint16_t* __restrict__ rel, uint32_t* __restrict__ count,
                             uint64_t* __restrict__ exitp, const uint32_t* __restrict__ bad_list,
                             uint32_t nbad) {
@@ -811,7 +830,7 @@ __global__ void k_chain_fix(const uint8_t* __restrict__ u, const uint64_t* __res
     while (b < nblk && entry[b] != exitp[b - 1]) {
       const uint64_t e = exitp[b - 1];
       entry[b] = e;
-      walk_one(u, uoff, b, e, hard_end, rel, count, exitp);
+      walk_one(u, uoff, b, e, hard_end, fmt, rel, count, exitp);
       ++b;
     }
     done_upto = b;

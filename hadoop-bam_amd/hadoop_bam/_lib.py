@@ -27,6 +27,8 @@ HBAM_EDEVICE = -10
 HBAM_EINVAL = -11
 HBAM_EMORE = -12
 HBAM_EINDEX = -13
+HBAM_ETRIBBLE = -14
+HBAM_ERUNTIME = -15
 
 CODE_NAMES = {
     HBAM_OK: "OK", HBAM_EIO: "IOException", HBAM_ETRUNC: "FileTruncatedException",
@@ -35,6 +37,7 @@ CODE_NAMES = {
     HBAM_EDATA: "RuntimeException(DataFormatException)", HBAM_ENOMEM: "OutOfMemory",
     HBAM_EUNSUPPORTED: "Unsupported", HBAM_EDEVICE: "DeviceError", HBAM_EINVAL: "InvalidArgument",
     HBAM_EMORE: "NeedMoreData", HBAM_EINDEX: "IndexOutOfBoundsException",
+    HBAM_ETRIBBLE: "TribbleException", HBAM_ERUNTIME: "RuntimeException",
 }
 
 # every entry point include/hbam.h declares (checked by tests/test_abi.py)
@@ -51,7 +54,8 @@ EXPORTS = [
     "hbam_summarize_ranges", "hbam_name_order", "hbam_fixmate", "hbam_download",
     "hbam_guess_window_len", "hbam_guess_windows", "hbam_guess_bgzf_window_len",
     "hbam_guess_bgzf_window", "hbam_probabilistic_splits_windows", "hbam_merge_remap",
-    "hbam_host_register", "hbam_host_unregister",
+    "hbam_host_register", "hbam_host_unregister", "hbam_bcf_parse_header", "hbam_guess_bcf_window_len",
+    "hbam_guess_bcf_windows", "hbam_bcf_decode_split",
 ]
 
 
@@ -99,6 +103,11 @@ class FixmateRunC(C.Structure):
                 ("offsets", C.c_void_p), ("payload", C.c_void_p)]
 
 
+class BcfHeaderC(C.Structure):
+    _fields_ = [("n_contig", C.c_int32), ("n_sample", C.c_int32), ("n_dict", C.c_int32),
+                ("bgzf", C.c_int32), ("header_len", C.c_uint64), ("first_voffset", C.c_uint64)]
+
+
 _u8p = C.POINTER(C.c_uint8)
 _u16p = C.POINTER(C.c_uint16)
 _u32p = C.POINTER(C.c_uint32)
@@ -118,6 +127,21 @@ class Columns(C.Structure):
         ("names", _u8p), ("cigar_off", _u64p), ("cigars", _u32p), ("seq_off", _u64p),
         ("seq", _u8p), ("qual", _u8p), ("aux_off", _u64p), ("aux", _u8p),
     ]
+
+
+class BcfColumnsC(C.Structure):
+    _fields_ = [
+        ("n_records", C.c_uint64), ("status", C.c_int32), ("pad0", C.c_int32),
+        ("err_record", C.c_uint64), ("rel", C.c_void_p), ("rec_off", C.c_void_p), ("data", C.c_void_p),
+        ("data_len", C.c_uint64), ("key", C.c_void_p), ("l_shared", C.c_void_p), ("l_indiv", C.c_void_p),
+        ("chrom", C.c_void_p), ("pos", C.c_void_p), ("rlen", C.c_void_p), ("qual", C.c_void_p),
+        ("n_allele_info", C.c_void_p), ("n_fmt_sample", C.c_void_p),
+    ]
+
+
+BCF_FIELDS = [("rel", np.int64), ("rec_off", np.uint64), ("key", np.int64), ("l_shared", np.int32),
+              ("l_indiv", np.int32), ("chrom", np.int32), ("pos", np.int32), ("rlen", np.int32),
+              ("qual", np.uint32), ("n_allele_info", np.int32), ("n_fmt_sample", np.int32)]
 
 
 FIXED = [("voffset", np.uint64), ("key", np.int64), ("rec_off", np.uint64),
@@ -197,6 +221,13 @@ def load(path=None):
         "hbam_host_register": (C.c_int, [vp, vp, C.c_uint64]),
         "hbam_host_unregister": (C.c_int, [vp, vp]),
         "hbam_bgzf_bound": (C.c_uint64, [C.c_uint64, C.c_uint32]),
+        "hbam_bcf_parse_header": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(BcfHeaderC)]),
+        "hbam_guess_bcf_window_len": (C.c_uint64, [C.c_uint64, C.c_int64, C.c_int64, C.c_int]),
+        "hbam_guess_bcf_windows": (C.c_int, [vp, vp, C.c_int, vp, C.c_uint64, vp, vp, C.c_uint64,
+                                             C.POINTER(BcfHeaderC), vp, vp]),
+        "hbam_bcf_decode_split": (C.c_int, [vp, vp, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
+                                            C.POINTER(BcfHeaderC), C.c_uint64, C.c_uint64,
+                                            C.POINTER(BcfColumnsC)]),
         "hbam_summarize_ranges": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(RangesC)]),
         "hbam_name_order": (C.c_int, [vp, vp, vp, C.c_uint64, vp]),
         "hbam_fixmate": (C.c_int, [vp, vp, vp, C.c_uint64, C.POINTER(FixmateRunC)]),
@@ -574,3 +605,59 @@ class Context:
                     src=self._d2h(r.src, k, np.uint32), mate=self._d2h(r.mate, k, np.uint32),
                     n_groups=int(r.n_groups), status=int(r.status))
 
+    # ---- BCF over BGZF --------------------------------------------------------
+    def bcf_parse_header(self, file_prefix):
+        """BCF2Codec.readHeader over the file's first bytes -> dict, or an error code."""
+        a = np.ascontiguousarray(np.frombuffer(bytes(file_prefix), np.uint8))
+        h = BcfHeaderC()
+        rc = self.L.hbam_bcf_parse_header(self.h, C.c_void_p(a.ctypes.data), a.size, C.byref(h))
+        if rc:
+            return rc
+        return dict(n_contig=h.n_contig, n_sample=h.n_sample, n_dict=h.n_dict, bgzf=bool(h.bgzf),
+                    header_len=h.header_len, first_voffset=h.first_voffset)
+
+    @staticmethod
+    def _bcf_hdr(h):
+        c = BcfHeaderC()
+        c.n_contig, c.n_sample, c.n_dict = h["n_contig"], h["n_sample"], h["n_dict"]
+        c.bgzf = int(bool(h["bgzf"]))
+        c.header_len = int(h["header_len"])
+        c.first_voffset = int(h.get("first_voffset", 0))
+        return c
+
+    def guess_bcf_window_len(self, file_len, beg, end, bgzf):
+        return int(self.L.hbam_guess_bcf_window_len(int(file_len), int(beg), int(end), int(bool(bgzf))))
+
+    def guess_bcf_windows(self, windows, win_off, file_len, beg, end, h):
+        """hbam_guess_bcf_windows: BCFSplitGuesser over the k windows -> (rc, out, err)."""
+        p, n, dev, keep = self._ptr(windows)
+        beg = np.ascontiguousarray(beg, np.int64)
+        end = np.ascontiguousarray(end, np.int64)
+        win_off = np.ascontiguousarray(win_off, np.uint64)
+        k = len(beg)
+        out = np.zeros(max(k, 1), np.int64)
+        err = np.zeros(max(k, 1), np.int32)
+        hc = self._bcf_hdr(h)
+        rc = self.L.hbam_guess_bcf_windows(self.h, p, dev, win_off.ctypes.data, int(file_len), beg.ctypes.data,
+                                           end.ctypes.data, k, C.byref(hc), out.ctypes.data, err.ctypes.data)
+        return rc, out[:k], err[:k]
+
+    def bcf_decode_split(self, data, h, start, end_or_len, comp_base=0, file_len=None, keep_data=False):
+        """BCFRecordReader over one split (hbam_bcf_decode_split) -> host numpy columns."""
+        p, n, dev, keep = self._ptr(data)
+        if file_len is None:
+            file_len = comp_base + n
+        d = BcfColumnsC()
+        hc = self._bcf_hdr(h)
+        rc = self.L.hbam_bcf_decode_split(self.h, p, dev, int(comp_base), n, int(file_len), C.byref(hc),
+                                          int(start), int(end_or_len), C.byref(d))
+        if rc:
+            return {"rc": rc, "error": self.last_error()}
+        k = int(d.n_records)
+        out = {"rc": 0, "n": k, "status": int(d.status), "err_record": int(d.err_record)}
+        for name, dt in BCF_FIELDS:
+            out[name] = self._d2h(getattr(d, name), k, dt)
+        if keep_data:
+            out["data"] = self._d2h(d.data, int(d.data_len), np.uint8)
+        out["timing"] = self.timing()
+        return out

@@ -15,6 +15,8 @@
  *   HBAM_EREFID       IllegalArgumentException (reference index not in dictionary)
  *   HBAM_EDATA        RuntimeException(java.util.zip.DataFormatException)
  *   HBAM_EINDEX       IndexOutOfBoundsException
+ *   HBAM_ETRIBBLE     htsjdk TribbleException (BCF)
+ *   HBAM_ERUNTIME     another RuntimeException out of BCF2Codec.decode (BCF, unpinned)
  *
  * Library-specific codes (no reference counterpart): HBAM_ENOMEM, HBAM_EUNSUPPORTED
  * (BGZF block with ISIZE > 65536), HBAM_EDEVICE (HIP error), HBAM_EINVAL, HBAM_EMORE
@@ -48,6 +50,8 @@ extern "C" {
 #define HBAM_EINVAL (-11)
 #define HBAM_EMORE (-12)
 #define HBAM_EINDEX (-13) /* IndexOutOfBoundsException (Summarize.java:715 on a record without a range) */
+#define HBAM_ETRIBBLE (-14) /* htsjdk TribbleException (BCF2Codec: unreadable / inconsistent BCF record) */
+#define HBAM_ERUNTIME (-15) /* another RuntimeException escaping BCF2Codec.decode (restated, unpinned) */
 
 typedef struct hbam_ctx hbam_ctx;
 
@@ -394,6 +398,66 @@ int hbam_fixmate(hbam_ctx* ctx, const uint8_t* ubuf, const uint64_t* rec_off, ui
  * above DEFLATE's 32768 (the pass refuses such a block instead of copying from outside it). */
 int hbam_resolve_tokens(hbam_ctx* ctx, uint8_t* io, uint32_t isize, const uint32_t* bitmap,
                         uint32_t tail_token, uint32_t tail_dist, int32_t* status);
+
+/* ---- BCF over BGZF ---------------------------------------------------- */
+/* BCF2Codec.readHeader: what the guesser and the record decode need from the header. */
+typedef struct hbam_bcf_header {
+  int32_t n_contig;       /* ##contig lines (BCF2Codec contigNames; CHROM indexes them) */
+  int32_t n_sample;       /* header.getNGenotypeSamples() */
+  int32_t n_dict;         /* string dictionary: PASS + FILTER/INFO/FORMAT IDs (BCF2Utils.makeDictionary) */
+  int32_t bgzf;           /* BlockCompressedInputStream.isValidFile(file) */
+  uint64_t header_len;    /* uncompressed bytes of magic, l_text and the header text */
+  uint64_t first_voffset; /* position of the first record: virtual offset (BGZF) or file offset */
+} hbam_bcf_header;
+
+/* BCFRecordReader output of one split (device memory owned by the context, valid until the
+ * next call on it).  Record i's bytes are data[rec_off[i], +8 + l_shared + l_indiv). */
+typedef struct hbam_bcf_columns {
+  uint64_t n_records;
+  int32_t status;       /* HBAM_OK, or the exception nextKeyValue() raises after n_records */
+  int32_t pad0;
+  uint64_t err_record;  /* == n_records */
+  int64_t* rel;         /* BGZF: uncompressed bytes from the split start; plain: file offset */
+  uint64_t* rec_off;    /* offset of the record's l_shared field in data */
+  uint8_t* data;        /* the record stream: inflated blocks (BGZF) or the file window (plain) */
+  uint64_t data_len;
+  int64_t* key;         /* BCFRecordReader key: (long)contig index << 32 | (long)(start - 1) */
+  int32_t* l_shared;
+  int32_t* l_indiv;
+  int32_t* chrom;
+  int32_t* pos;         /* 0-based POS */
+  int32_t* rlen;
+  uint32_t* qual;       /* QUAL float bits */
+  int32_t* n_allele_info;
+  int32_t* n_fmt_sample;
+} hbam_bcf_columns;
+
+/* BCF2Codec.readHeader over the file's first `len` bytes (BGZF blocks inflated on the device).
+ * HBAM_EMORE: the header runs past len.  Replaces BCFSplitGuesser.java:91-113 / BCFRecordReader
+ * .initContigDict :125-133. */
+int hbam_bcf_parse_header(hbam_ctx* ctx, const uint8_t* file, uint64_t len, hbam_bcf_header* out);
+
+/* Bytes BCFSplitGuesser.guessNextBCFRecordStart(beg, end) reads (BCFSplitGuesser.java:133-145):
+ * min((int)(end-beg), 2*0xffff+0xfffe) for BGZF, min(.., 0x80000) uncompressed, cut at EOF. */
+uint64_t hbam_guess_bcf_window_len(uint64_t file_len, int64_t beg, int64_t end, int bgzf);
+
+/* k guessNextBCFRecordStart calls over caller-gathered windows (window i =
+ * windows[win_off[i], win_off[i+1]) = exactly hbam_guess_bcf_window_len bytes from beg[i]).
+ * out[i]: virtual offset (BGZF) / file offset (plain) of the guessed record, or end[i];
+ * err[i]: the exception escaping the guesser (HBAM_OK normally).  Replaces
+ * BCFSplitGuesser.java:128-281 as called by VCFInputFormat.addGuessedSplits :269. */
+int hbam_guess_bcf_windows(hbam_ctx* ctx, const uint8_t* windows, int on_device, const uint64_t* win_off,
+                           uint64_t file_len, const int64_t* beg, const int64_t* end, uint64_t k,
+                           const hbam_bcf_header* h, int64_t* out, int32_t* err);
+
+/* BCFRecordReader over one split (BCFRecordReader.java:71-174): BGZF -> FileVirtualSplit
+ * [v_start, v_end) read through BGZFLimitingStream (:177-237); plain -> FileSplit start =
+ * v_start, length = v_end.  comp = file bytes [comp_base, file_len) (a BCF split reads to the
+ * end of the file).  The record decode is a restated subset of htsjdk's BCF2Codec (parity
+ * unpinned; oracle/hbam_oracle_bcf.c lists the rules). */
+int hbam_bcf_decode_split(hbam_ctx* ctx, const uint8_t* comp, int on_device, uint64_t comp_base,
+                          uint64_t comp_len, uint64_t file_len, const hbam_bcf_header* h, uint64_t v_start,
+                          uint64_t v_end, hbam_bcf_columns* out);
 
 #ifdef __cplusplus
 }

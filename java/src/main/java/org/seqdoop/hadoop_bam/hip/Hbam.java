@@ -15,7 +15,7 @@ import htsjdk.samtools.util.RuntimeIOException;
 
 public final class Hbam implements AutoCloseable {
   public static final int OK = 0, EIO = -1, ETRUNC = -2, EFORMAT = -3, ERUNTIMEIO = -4,
-      EEOF = -5, EREFID = -6, EDATA = -7, EMORE = -12, EINDEX = -13;
+      EEOF = -5, EREFID = -6, EDATA = -7, EMORE = -12, EINDEX = -13, ETRIBBLE = -14, ERUNTIME = -15;
 
   private static final Linker LINKER = Linker.nativeLinker();
   private static final SymbolLookup LIB = SymbolLookup.libraryLookup(
@@ -70,6 +70,25 @@ public final class Hbam implements AutoCloseable {
   static final MethodHandle NAME_ORDER = fn("hbam_name_order", FunctionDescriptor.of(I, A, A, A, J, A));
   static final MethodHandle FIXMATE = fn("hbam_fixmate", FunctionDescriptor.of(I, A, A, A, J, A));
   static final MethodHandle DOWNLOAD = fn("hbam_download", FunctionDescriptor.of(I, A, A, J, A));
+  // SURVEY.md §8 f-3: BCF over BGZF (HipBCFSplitGuesser, HipBCFRecordReader)
+  static final MethodHandle BCF_PARSE_HEADER = fn("hbam_bcf_parse_header", FunctionDescriptor.of(I, A, A, J, A));
+  static final MethodHandle GUESS_BCF_WINDOW_LEN = fn("hbam_guess_bcf_window_len",
+      FunctionDescriptor.of(J, J, J, J, I));
+  static final MethodHandle GUESS_BCF_WINDOWS = fn("hbam_guess_bcf_windows",
+      FunctionDescriptor.of(I, A, A, I, A, J, A, A, J, A, A, A));
+  static final MethodHandle BCF_DECODE_SPLIT = fn("hbam_bcf_decode_split",
+      FunctionDescriptor.of(I, A, A, I, J, J, J, A, J, J, A));
+
+  /** hbam_bcf_header: n_contig, n_sample, n_dict, bgzf, header_len, first_voffset (32 bytes). */
+  public static final StructLayout BCF_HEADER = MemoryLayout.structLayout(
+      I.withName("n_contig"), I.withName("n_sample"), I.withName("n_dict"), I.withName("bgzf"),
+      J.withName("header_len"), J.withName("first_voffset"));
+  /** hbam_bcf_columns: counts/status, then rel, rec_off, data, data_len and the field arrays. */
+  public static final StructLayout BCF_COLUMNS = MemoryLayout.structLayout(
+      J.withName("n_records"), I.withName("status"), I.withName("pad0"), J.withName("err_record"),
+      A.withName("rel"), A.withName("rec_off"), A.withName("data"), J.withName("data_len"), A.withName("key"),
+      A.withName("l_shared"), A.withName("l_indiv"), A.withName("chrom"), A.withName("pos"), A.withName("rlen"),
+      A.withName("qual"), A.withName("n_allele_info"), A.withName("n_fmt_sample"));
 
   /** hbam_ranges: n, status, pad, then the key / beg / end / rev / record device arrays. */
   public static final StructLayout RANGES = MemoryLayout.structLayout(
@@ -122,6 +141,8 @@ public final class Hbam implements AutoCloseable {
       case EDATA: return new RuntimeException(new java.util.zip.DataFormatException(where));
       case EIO: return new RuntimeIOException(new IOException(where));
       case EINDEX: return new IndexOutOfBoundsException(where);
+      case ETRIBBLE: return new htsjdk.tribble.TribbleException(where);
+      case ERUNTIME: return new RuntimeException("BCF2Codec.decode: " + where);
       default: return new RuntimeIOException("hbam error " + code + " at " + where);
     }
   }

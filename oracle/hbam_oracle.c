@@ -1078,3 +1078,6 @@ void or_cols_free(or_cols* c) {
   free(c->var);
   memset(c, 0, sizeof *c);
 }
+
+/* BCF read path: shares the stream model above */
+#include "hbam_oracle_bcf.c"

@@ -32,7 +32,9 @@ enum {
   OR_EEOF = -5,       /* htsjdk RuntimeEOFException */
   OR_EREFID = -6,     /* IllegalArgumentException (reference index not in dictionary) */
   OR_EDATA = -7,      /* RuntimeException wrapping java.util.zip.DataFormatException */
-  OR_ENOMEM = -8      /* host allocation failure (never modelled as OOM) */
+  OR_ENOMEM = -8,     /* host allocation failure (never modelled as OOM) */
+  OR_ETRIBBLE = -9,   /* htsjdk TribbleException (BCF2Codec) */
+  OR_ERUNTIME = -10   /* another RuntimeException escaping BCF2Codec.decode (unpinned) */
 };
 
 /* MurmurHash3.murmurhash3(byte[], int) — util/MurmurHash3.java:32-102 */
@@ -162,6 +164,22 @@ void or_name_order(const uint8_t* pay, const uint64_t* off, uint64_t n, uint32_t
 /* FixMateReducer (FixMate.java:230-277) over the shuffle order: the reducer's writes */
 int64_t or_fixmate(const uint8_t* pay, const uint64_t* off, uint64_t n, uint8_t* out_pay, uint64_t* out_off,
                    uint32_t* out_src, uint64_t cap, uint64_t pay_cap, int32_t* status);
+
+/* ---- BCF, hbam_oracle_bcf.c ---------------------------------------- */
+/* BCF2Codec.readHeader of uncompressed stream bytes: contig count, sample count, string
+ * dictionary size, bytes of magic + l_text + text.  OR_EEOF: more bytes needed. */
+int or_bcf_read_header(const uint8_t* u, uint64_t n, int32_t* n_contig, int32_t* n_sample,
+                       int32_t* n_dict, uint64_t* header_len);
+/* BCFSplitGuesser.guessNextBCFRecordStart (BCFSplitGuesser.java:128-281) over the whole file */
+int64_t or_guess_bcf_record_start(const uint8_t* f, uint64_t len, int64_t beg, int64_t end, int is_bgzf,
+                                  int32_t n_contig, int32_t n_sample, int32_t n_dict, int* err);
+/* BCFRecordReader over one split (BGZF: FileVirtualSplit [v_start, v_end); uncompressed:
+ * FileSplit start = v_start, length = v_end).  rel: record position (BGZF: uncompressed bytes
+ * from the split start; uncompressed: file offset). */
+int64_t or_read_bcf_split(const uint8_t* f, uint64_t len, int is_bgzf, uint64_t v_start, uint64_t v_end,
+                          int32_t n_contig, int32_t n_sample, int32_t n_dict, uint64_t header_len,
+                          int64_t* rel, int32_t* chrom, int32_t* pos, int64_t* key, uint64_t cap,
+                          int* status);
 
 #ifdef __cplusplus
 }

@@ -70,6 +70,16 @@ def lib():
         L.or_fixmate.restype = C.c_int64
         L.or_fixmate.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint64, C.c_uint64,
                                  C.POINTER(C.c_int32)]
+        L.or_bcf_read_header.restype = C.c_int
+        L.or_bcf_read_header.argtypes = [u8p, C.c_uint64, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
+        L.or_guess_bcf_record_start.restype = C.c_int64
+        L.or_guess_bcf_record_start.argtypes = [u8p, C.c_uint64, C.c_int64, C.c_int64, C.c_int,
+                                                C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int)]
+        L.or_read_bcf_split.restype = C.c_int64
+        L.or_read_bcf_split.argtypes = [u8p, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_int32,
+                                        C.c_int32, C.c_int32, C.c_uint64, vp, vp, vp, vp, C.c_uint64,
+                                        C.POINTER(C.c_int)]
         _LIB = L
     return _LIB
 
@@ -462,3 +472,101 @@ def fixmate(payload, offsets):
                          src.ctypes.data, cap, pay_cap, C.byref(st))
     assert k >= 0, k
     return dict(payload=out[:int(ooff[k])], offsets=ooff[:k + 1], src=src[:k], status=st.value)
+
+
+# ---- BCF: hbam_oracle_bcf.c -------------------------------------------------
+def is_bgzf(data):
+    """BlockCompressedInputStream.isValidFile: an 18-byte BGZF member header at offset 0."""
+    b = bytes(data[:18])
+    return (len(b) == 18 and b[:4] == b"\x1f\x8b\x08\x04" and b[10:12] == b"\x06\x00"
+            and b[12:14] == b"BC" and b[14:16] == b"\x02\x00")
+
+
+def bcf_stream_prefix(data, want=1 << 20):
+    """Uncompressed stream bytes at the start of a (BGZF or plain) BCF file."""
+    if not is_bgzf(data):
+        return bytes(data[:want])
+    out, p = [], 0
+    n = 0
+    while p + 18 <= len(data) and n < want:
+        bl = int.from_bytes(bytes(data[p + 16:p + 18]), "little") + 1
+        rc, u = inflate_block(bytes(data[p:p + bl]), check_crc=False)
+        if rc:
+            break
+        out.append(u)
+        n += len(u)
+        p += bl
+    return b"".join(out)
+
+
+def bcf_header(data):
+    """BCF2Codec.readHeader: dict(n_contig, n_sample, n_dict, header_len, bgzf) or an error code."""
+    u = bcf_stream_prefix(data)
+    a, p = _buf(u if u else b"\0")
+    nc, ns, nd, hl = C.c_int32(), C.c_int32(), C.c_int32(), C.c_uint64()
+    rc = lib().or_bcf_read_header(p, len(u), C.byref(nc), C.byref(ns), C.byref(nd), C.byref(hl))
+    if rc:
+        return rc
+    return dict(n_contig=nc.value, n_sample=ns.value, n_dict=nd.value, header_len=hl.value,
+                bgzf=is_bgzf(data))
+
+
+def guess_bcf_record_start(data, beg, end, h):
+    """BCFSplitGuesser.guessNextBCFRecordStart -> (guess, err)."""
+    a, p = _buf(data)
+    err = C.c_int(0)
+    r = lib().or_guess_bcf_record_start(p, len(a), beg, end, int(h["bgzf"]), h["n_contig"],
+                                        h["n_sample"], h["n_dict"], C.byref(err))
+    return r, err.value
+
+
+def read_bcf_split(data, start, end_or_len, h, cap=1 << 22):
+    """BCFRecordReader over one split: BGZF -> FileVirtualSplit [start, end_or_len) (virtual);
+    uncompressed -> FileSplit start, length = end_or_len.  dict(n, status, rel, chrom, pos, key)."""
+    a, p = _buf(data)
+    rel = np.zeros(cap, np.int64)
+    chrom = np.zeros(cap, np.int32)
+    pos = np.zeros(cap, np.int32)
+    key = np.zeros(cap, np.int64)
+    st = C.c_int(0)
+    n = lib().or_read_bcf_split(p, len(a), int(h["bgzf"]), start, end_or_len, h["n_contig"],
+                                h["n_sample"], h["n_dict"], h["header_len"], rel.ctypes.data,
+                                chrom.ctypes.data, pos.ctypes.data, key.ctypes.data, cap, C.byref(st))
+    n = int(n)
+    m = min(n, cap)
+    return dict(n=n, status=st.value, rel=rel[:m].copy(), chrom=chrom[:m].copy(), pos=pos[:m].copy(),
+                key=key[:m].copy())
+
+
+def bcf_splits(data, split_size, h):
+    """VCFInputFormat.addGuessedSplits for one BCF path (VCFInputFormat.java:241-310) over
+    FileInputFormat's splits of split_size: list of (start, end) — virtual offsets for BGZF
+    (FileVirtualSplit), (start, length) for uncompressed (FileSplit); or an error code
+    (OR_EIO: "no records in first split", or the guesser's escaping exception)."""
+    n = len(data)
+    fs = []
+    b = 0
+    while n - b > 1.1 * split_size:  # FileInputFormat SPLIT_SLOP
+        fs.append((b, split_size))
+        b += split_size
+    if n - b > 0:
+        fs.append((b, n - b))
+    out = []
+    bg = bool(h["bgzf"])
+    for beg, ln in fs:
+        end = beg + ln
+        g, err = guess_bcf_record_start(data, beg, end, h)
+        if err:
+            return err
+        align_end = (end << 16 | 0xffff) if bg else end
+        if g == end:
+            if not out:
+                return -1
+            if bg:
+                out[-1] = (out[-1][0], align_end)
+                continue
+            prev = out.pop()
+            out.append((g, align_end - g))  # the reference's FileSplit(path, alignBeg, length)
+            continue
+        out.append((g, align_end) if bg else (g, align_end - g))
+    return out

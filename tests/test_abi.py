@@ -67,9 +67,10 @@ def test_struct_layouts_match_the_header():
 #include <stdio.h>
 #include "hbam.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(hbam_columns), offsetof(hbam_columns, voffset),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(hbam_columns), offsetof(hbam_columns, voffset),
          offsetof(hbam_columns, ubuf_len), offsetof(hbam_columns, aux), sizeof(hbam_sorted_run),
-         sizeof(hbam_timing));
+         sizeof(hbam_timing), sizeof(hbam_bcf_header), sizeof(hbam_bcf_columns),
+         offsetof(hbam_bcf_columns, data_len), offsetof(hbam_bcf_columns, n_fmt_sample));
   return 0;
 }'''
     with tempfile.TemporaryDirectory() as d:
@@ -82,14 +83,20 @@ int main(void) {
     assert got[1] == _lib.Columns.voffset.offset and got[2] == _lib.Columns.ubuf_len.offset
     assert got[3] == _lib.Columns.aux.offset
     assert got[4] == C.sizeof(_lib.SortedRunC) and got[5] == C.sizeof(_lib.Timing)
+    assert got[6] == C.sizeof(_lib.BcfHeaderC) == 32 and got[7] == C.sizeof(_lib.BcfColumnsC)
+    assert got[8] == _lib.BcfColumnsC.data_len.offset and got[9] == _lib.BcfColumnsC.n_fmt_sample.offset
     # the Java shim: 4 header fields, then 27 pointer-sized slots in the header's order
     java = open(os.path.join(ROOT, "java", "src", "main", "java", "org", "seqdoop", "hadoop_bam",
                              "hip", "Hbam.java")).read()
-    body = java[java.index("COLUMNS = MemoryLayout.structLayout("):]
-    body = body[:body.index(");")]
-    names = re.findall(r'withName\("(\w+)"\)', body)
+
+    def layout(name):
+        body = java[java.index("StructLayout %s = MemoryLayout.structLayout(" % name):]
+        return re.findall(r'withName\("(\w+)"\)', body[:body.index(");")])
+    names = layout("COLUMNS")
     assert names == [f[0] for f in _lib.Columns._fields_]
     assert len(names) - 4 == 27
+    assert layout("BCF_COLUMNS") == [f[0] for f in _lib.BcfColumnsC._fields_]
+    assert layout("BCF_HEADER") == [f[0] for f in _lib.BcfHeaderC._fields_]
 
 
 _C2J = {"void": None}
