@@ -235,9 +235,6 @@ __global__ void k_edge_merge(const BlockRec* __restrict__ blk, const uint64_t* _
 }
 
 // LZ77 resolution of one block (phase 2 of the batched inflate); see resolve_dev.h.
-#ifndef HBAM_RS_LATE_WB
-#define HBAM_RS_LATE_WB 1  // A/B knob: stretch write-back issued after the raw prefetch
-#endif
 // one 16-byte column of a resolved stretch -> ubuf (bytewise where it overlaps a neighbour block)
 __device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64_t a, uint64_t base,
                                               uint64_t aend, const uint4 v) {
@@ -250,9 +247,6 @@ __device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64
     }
   }
 }
-#ifndef HBAM_RS_SERIAL
-#define HBAM_RS_SERIAL 1  // ordered matches: round 1 in parallel, the rest in order on one lane
-#endif
 #ifndef HBAM_RS_WAVES
 // waves per SIMD asked of the register allocator: 8 = the hardware maximum, which the 4.9 KiB of
 // LDS per block also allows (VGPRs 75 -> 64, 2 spilled): k_resolve 47.4 -> 42.6 ms at 10 GB
@@ -270,9 +264,7 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
   __shared__ uint32_t s_rec[RS_MAXM];
   __shared__ uint16_t s_pos[RS_MAXM];
   __shared__ uint64_t s_sel[8];
-#ifndef HBAM_RS_PREFIX
   __shared__ uint32_t s_pend[RS_PW];
-#endif
   const uint32_t b = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   if (b >= nblk) return;
@@ -396,9 +388,8 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
     // previous stretch's write-back region); a source older than that is read from ubuf
     // (stretches <= k-2, written back at least one iteration ago; the drain below makes that
     // explicit), and a source that straddles the boundary is copied in two parts.
-#ifndef HBAM_RS_NODRAIN  // A/B at 10 GB without the drain: 58.8 vs 58.6 ms, so it stays
+    // (A/B at 10 GB without this drain: 58.8 vs 58.6 ms, so it stays)
     if (s0 >= RS_W) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     const uint32_t lds_from = s0 - RS_W - a0;  // block offset of LDS index 0 (when s0 >= RS_W)
     for (uint32_t j = lane; j < npre; j += 64) {
       const uint64_t rec = rs_unpack(s_rec[j], s_pos);
@@ -416,7 +407,6 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
 #ifdef HBAM_PROF
     p_pre += PROF_CLK() - q1;
 #endif
-#ifndef HBAM_RS_PREFIX
     // ---- ordered matches: dataflow rounds.  s_pend holds one bit per byte of the stretch
     // (+ match spill) that an ordered match has yet to write; a match is ready when no byte of
     // its external source [p - dist, p - dist + min(len, dist)) is pending.  Every round
@@ -451,61 +441,6 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
         rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
         rs_bits(s_pend, p - s0, len, false);
       };
-#if HBAM_RS_SERIAL
-      // Round 1 on every lane: the matches whose source has no pending byte (60 % of the
-      // ordered ones on BAM data).  The rest then run in program order on one lane: a pending
-      // byte of a match's source is written by a match that starts before it, so in-order
-      // execution only ever reads final bytes.  The dataflow rounds this replaces took 4.4
-      // rounds per stretch (295 per block, each ~3.7 k cycles of LDS latency) for the ~13
-      // matches per stretch left after round 1 (tools/rounds_sim.py).
-      uint32_t ready = (live & 1u) && is_ready(rec0) ? 1u : 0u;
-#pragma unroll 1
-      for (uint32_t t = 1; t < mine; ++t)
-        if ((live >> t & 1u) && is_ready(rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos))) ready |= 1u << t;
-      rs_lds_order();
-      if (ready & 1u) {
-        const uint32_t p = (uint32_t)rec0 & 0xffffu, len = (uint32_t)(rec0 >> 16) & 0xffffu,
-                       dist = (uint32_t)(rec0 >> 32) & 0xffffu;
-        rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
-      }
-#pragma unroll 1
-      for (uint32_t t = 1; t < mine; ++t)
-        if (ready >> t & 1u) {
-          const uint64_t rec = rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos);
-          rs_copy_lds(s_buf, lbase + ((uint32_t)rec & 0xffffu), (uint32_t)(rec >> 16) & 0xffffu,
-                      (uint32_t)(rec >> 32) & 0xffffu, s_sel);
-        }
-      live &= ~ready;
-#ifdef HBAM_PROF
-      ++n_bat;
-#endif
-      if (__any(live != 0u)) {
-        // which ordered matches round 1 ran: bit j of s_pend[2t .. 2t+1] for match j = lane + 64t
-        // (the pending bitmap is not needed any more)
-        const uint32_t nslot = (nord + 63u) / 64u;
-#pragma unroll 1
-        for (uint32_t t = 0; t < nslot; ++t) {
-          const uint64_t m = __ballot(t < mine && (ready >> t & 1u));
-          if (lane == 0) {
-            s_pend[2 * t] = (uint32_t)m;
-            s_pend[2 * t + 1] = (uint32_t)(m >> 32);
-          }
-        }
-        rs_lds_order();
-        if (lane == 0) {
-#pragma unroll 1
-          for (uint32_t j = 0; j < nord; ++j) {
-            if (s_pend[j >> 5] >> (j & 31u) & 1u) continue;
-            const uint64_t rec = rs_unpack(s_rec[RS_MAXM - 1 - j], s_pos);
-            rs_copy_lds(s_buf, lbase + ((uint32_t)rec & 0xffffu), (uint32_t)(rec >> 16) & 0xffffu,
-                        (uint32_t)(rec >> 32) & 0xffffu, s_sel);
-          }
-        }
-#ifdef HBAM_PROF
-        ++n_bat;
-#endif
-      }
-#else
       for (;;) {
         uint32_t ready = (live & 1u) && is_ready(rec0) ? 1u : 0u;
 #pragma unroll 1
@@ -527,32 +462,7 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
         }
         rs_lds_order();
       }
-    #endif  // HBAM_RS_SERIAL
     }
-#else
-    // ---- ordered matches: in-order batches
-    for (uint32_t kk = 0; kk < nord;) {
-      const uint32_t j = kk + lane;
-      const uint64_t rec = j < nord ? rs_unpack(s_rec[RS_MAXM - 1 - j], s_pos) : ~0ULL;
-      const uint32_t pk = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)rec & 0xffffu);
-      const bool ready = (j < nord) && (uint32_t)(rec >> 48) <= pk;
-      const uint64_t nr = __ballot(!ready);
-      const uint32_t c = nr ? (uint32_t)(__ffsll((unsigned long long)nr) - 1) : 64u;
-      if (c == 0u) {  // no progress possible (validated descriptors always make some): corrupt
-        if (lane == 0) status[b] = INF_DATA;
-        return;
-      }
-      if (lane < c) {
-        const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
-                       dist = (uint32_t)(rec >> 32) & 0xffffu;
-        rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
-      }
-      kk += c;
-#ifdef HBAM_PROF
-      ++n_bat;
-#endif
-    }
-#endif
     if ((tail0 & 0x80000000u) && (tail0 & 0xffffu) / RS_S == k && lane == 0) {
       // final match shorter than 3 bytes (the output filled up inside it); last token
       const uint32_t p = tail0 & 0xffffu, n = (tail0 >> 16) & 0x7fffu;
@@ -582,10 +492,6 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
     uint4 wbv[RS_C];
 #pragma unroll
     for (uint32_t h = 0; h < RS_C; ++h) wbv[h] = *(const uint4*)(s_buf + RS_W + 1024u * h + 16u * lane);
-#if !HBAM_RS_LATE_WB
-#pragma unroll
-    for (uint32_t h = 0; h < RS_C; ++h) rs_write_back(ubuf, abase + s0 + 1024u * h + 16u * lane, base, aend, wbv[h]);
-#endif
     // move [RS_S, RS_S + RS_W + RS_S) down to 0 in 16-byte columns; one wave, so every read of
     // a 1 KiB step lands before that step's writes (any RS_W that is a multiple of 16)
 #pragma unroll
@@ -594,10 +500,8 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
     *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = ra0;
     if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = ra1;
     load_raw(k + 3, ra0, ra1);
-#if HBAM_RS_LATE_WB
 #pragma unroll
     for (uint32_t h = 0; h < RS_C; ++h) rs_write_back(ubuf, abase + s0 + 1024u * h + 16u * lane, base, aend, wbv[h]);
-#endif
     __syncthreads();
 #ifdef HBAM_PROF
     p_wb += PROF_CLK() - q2;

@@ -52,25 +52,10 @@ constexpr uint32_t TOK_K = HBAM_TOK_K;
 #ifndef HBAM_TOK_DOT2
 #define HBAM_TOK_DOT2 1  // dot2 accumulation in the packed lookup: 68.5 -> 67.5 ms at 10 GB (profiles/r02/s2/ab_dot2_10g.txt)
 #endif
-#ifndef HBAM_TOK_PRED
-// fast path as one predicated path (tok_fast_pred) instead of the branching tok_fast: with plain
-// token stores 69.9 -> 67.9 ms at 10 GB (profiles/r02/s2/ab_pred_plainstores_10g.txt).  The
-// cycle-stamp profiling build keeps the branching path: with the stamps in the loop, the
-// predicated one reported DataFormatException on 11k of 78k blocks of a 2 GB file that the
-// shipped build inflates CRC-clean (tools/check_inflate_crc.py: 8 files, 283k blocks, 0
-// mismatches), so the profile of that build would not describe the shipped kernel anyway.
-#ifdef HBAM_PROF
-#define HBAM_TOK_PRED 0
-#else
-#define HBAM_TOK_PRED 1
-#endif
-#endif
-#ifndef HBAM_TOK_SPEC
-// fast path tok_fast_spec: decode first, then the iteration's output as one packet (TSink::put):
-// 66.4 -> 60.3 ms at 10 GB (profiles/r02/s2/ab_spec_10g.txt; the same decode order with the
-// three separate sink calls: 66.7 ms)
-#define HBAM_TOK_SPEC 1
-#endif
+// The fast path (tok_fast_spec): up to two literals and a match per iteration, decoded first
+// (both lit/len lookups before either LDS symbol read), then written as one packet
+// (TSink::put): 66.4 -> 60.3 ms at 10 GB against the same decode with one sink call per token
+// (profiles/r02/s2/ab_spec_10g.txt).
 // stream bits one fast-path iteration may consume: 2 lit/len codes + length extra + distance
 // code + distance extra = 15+15+5+15+13 = 63 (<= 64)
 constexpr uint32_t TOK_FAST_BITS = 64u;
@@ -79,16 +64,7 @@ constexpr uint32_t TOK_LENS_D = 320;    //               distance code lengths a
 
 // ---- input: two register banks + one quad in flight ------------------------------------
 typedef const __attribute__((address_space(1))) u32x4_t* gq_ptr;  // global (not flat) loads
-#ifndef HBAM_TOK_NTLOAD
-#define HBAM_TOK_NTLOAD 0  // A/B: non-temporal compressed-input loads (L2 traffic of the pass)
-#endif
-__device__ __forceinline__ u32x4_t ein_load(const uint4* p) {
-#if HBAM_TOK_NTLOAD
-  return __builtin_nontemporal_load((gq_ptr)p);
-#else
-  return *(gq_ptr)p;
-#endif
-}
+__device__ __forceinline__ u32x4_t ein_load(const uint4* p) { return *(gq_ptr)p; }
 struct EIn {
   const uint4* fp;    // quad held in t (merged at the next epoch); == fend when the fetch is done
   const uint4* fend;  // one past the last quad that holds stream bytes
@@ -391,47 +367,12 @@ struct TSink {
     }
     mark(op);
   }
-#if HBAM_TOK_PRED
-  // Predicated forms (A/B): the call is made by every lane of the iteration and `en` says
-  // whether it writes; only the chunk flush (a store) sits behind a branch.
+  // chunk switch as a predicated step: only the flush (a store) sits behind a branch
   __device__ __forceinline__ void switch_if(bool sw, uint32_t c) {
     if (sw) flush();
     curc = sw ? c : curc;
     lo = sw ? 0ull : lo;
     hi = sw ? 0ull : hi;
-  }
-  __device__ __forceinline__ void literal_if(bool en, uint32_t op, uint32_t b) {
-    const uint32_t r = soff + op, c = r >> 4;
-    switch_if(en && c != curc, c);
-    const uint64_t v = en ? (uint64_t)(b & 0xffu) << ((r & 7u) << 3) : 0ull;
-    const bool h = (r & 8u) != 0u;
-    hi |= h ? v : 0ull;
-    lo |= h ? 0ull : v;
-  }
-  __device__ __forceinline__ void match_if(bool en, uint32_t op, uint32_t n, uint32_t dist) {
-    if (en && n < 3u) {
-      tail[0] = op | n << 16 | 0x80000000u;
-      tail[1] = dist;
-    }
-    const bool em = en && n >= 3u;
-    const uint64_t d = em ? (uint64_t)((n - 3u) | (dist - 1u) << 8) : 0ull;
-    const uint32_t r = soff + op;
-    const uint32_t c = r >> 4, k = r & 15u;
-    switch_if(em && c != curc, c);
-    // every shift amount stays below 64 whichever arm the select keeps (a shift by 64 is
-    // undefined even when its result is discarded, and the optimizer may exploit it)
-    const uint32_t kl = k < 8u ? k : 0u, kh = k < 8u ? 0u : k - 8u;
-    const uint32_t kr = (k > 5u && k < 8u) ? 64u - 8u * k : 8u;
-    lo |= k < 8u ? d << (8u * kl) : 0ull;
-    hi |= (k < 8u && k > 5u) ? d >> kr : 0ull;
-    hi |= k < 8u ? 0ull : d << (8u * kh);
-    const bool sp = em && k >= 14u;
-    if (sp) flush();
-    const uint64_t spill = d >> (8u * (16u - (k >= 14u ? k : 14u)));
-    curc = sp ? c + 1u : curc;
-    lo = sp ? spill : lo;
-    hi = sp ? 0ull : hi;
-    if (em) mark(op);
   }
   // One iteration's output as one packet: nb (<= 5) bytes P (LSB first) at ubuf position
   // soff + op: up to two literals and a 3-byte match descriptor, always contiguous, so one
@@ -454,7 +395,6 @@ struct TSink {
     lo = sp ? spill : lo;
     hi = sp ? 0ull : hi;
   }
-#endif
   __device__ __forceinline__ void finish() {
     flush();
     while (bwin < nwin) {
@@ -557,123 +497,15 @@ __device__ __attribute__((noinline)) bool tok_build(const uint8_t* __restrict__ 
 
 // One iteration of the symbol loop with >= 64 stream bits left: two lit/len codes + length
 // extra + distance code + distance extra (15+15+5+15+13) fit, so zlib's end-of-input outcomes
-// cannot occur and after one refill (>= 33 bits in bb) none is checked.  A literal is
-// followed by a second lit/len decode in the same iteration: the wave pays for the match path
-// once per iteration either way, and most symbols are literals.
+// cannot occur and after one refill (>= 33 bits in bb) none is checked.  A literal is followed
+// by a second lit/len decode in the same iteration (the wave pays for the match path once per
+// iteration either way, and most symbols are literals).  Every lane runs the whole iteration
+// and flags say which of its results count (SIMT runs the union of the paths anyway); the
+// first exit code a lane meets wins, as zlib's early returns.  Both lit/len lookups run before
+// either symbol read (the second on the bits after the first code, whether or not it turns out
+// to be used), so the two LDS reads are in flight together; the iteration's bytes (up to two
+// literals and a match descriptor, contiguous) go to the sink as one packet.
 // Returns 0 next, 1 end of block, 2 output full (zlib stops), 3 data error.
-__device__ __forceinline__ uint32_t tok_fast(EIn& in, const HuffP& hl, const HuffP& hd,
-                                             const uint8_t* __restrict__ syms_ll,
-                                             const uint8_t* __restrict__ syms_d, TSink& sink,
-                                             uint32_t& op, uint32_t isize) {
-  ein_refill(in);
-  uint32_t L, idx, hi = 0;
-  if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) return 3u;
-  uint32_t sym = (uint32_t)syms_ll[idx] | hi;
-  ein_drop(in, L);
-  if (sym < 256u) {
-    if (op == isize) return 2u;
-    sink.literal(op++, sym);
-    if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) return 3u;
-    sym = (uint32_t)syms_ll[idx] | hi;
-    ein_drop(in, L);
-    if (sym < 256u) {
-      if (op == isize) return 2u;
-      sink.literal(op++, sym);
-      return 0u;
-    }
-  }
-  if (sym == 256u) return 1u;
-  if (sym > 285u) return 3u;
-  uint32_t lbase, lext;
-  length_base(sym, lbase, lext);
-  ein_refill(in);
-  const uint32_t mlen = lbase + ein_peek(in, lext);
-  ein_drop(in, lext);
-  uint32_t dh;
-  if (!huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh)) return 3u;
-  const uint32_t dsym = syms_d[idx];
-  ein_drop(in, L);
-  if (dsym > 29u) return 3u;
-  uint32_t dbase, dext;
-  dist_base(dsym, dbase, dext);
-  const uint32_t dist = dbase + ein_peek(in, dext);
-  ein_drop(in, dext);
-  if (op == isize) return 2u;
-  if (dist > op) return 3u;
-  uint32_t n = isize - op;
-  n = mlen < n ? mlen : n;
-  sink.match(op, n, dist);
-  op += n;
-  return n < mlen ? 2u : 0u;
-}
-#if HBAM_TOK_PRED
-// tok_fast as one predicated path (A/B): same outcomes and precedence; the first exit code a
-// lane meets wins, as the original's early returns.
-__device__ __forceinline__ uint32_t tok_fast_pred(EIn& in, const HuffP& hl, const HuffP& hd,
-                                                  const uint8_t* __restrict__ syms_ll,
-                                                  const uint8_t* __restrict__ syms_d, TSink& sink,
-                                                  uint32_t& op, uint32_t isize) {
-  ein_refill(in);
-  uint32_t ex = 0;
-  uint32_t L, idx, hi = 0;
-  const bool ok1 = huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi);
-  const uint32_t sym1 = ((uint32_t)syms_ll[ok1 ? idx : 0u] | hi);
-  ex = ok1 ? 0u : 3u;
-  ein_drop(in, ok1 ? L : 0u);
-  const bool lit1 = ok1 && sym1 < 256u;
-  ex = (ex == 0u && lit1 && op == isize) ? 2u : ex;
-  const bool emit1 = ex == 0u && lit1;
-  sink.literal_if(emit1, op, sym1);
-  op += emit1 ? 1u : 0u;
-  const bool ok2 = huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi);
-  const uint32_t sym2 = ((uint32_t)syms_ll[ok2 ? idx : 0u] | hi);
-  ex = (emit1 && !ok2) ? 3u : ex;
-  ein_drop(in, (emit1 && ok2) ? L : 0u);
-  const bool lit2 = emit1 && ok2 && sym2 < 256u;
-  ex = (ex == 0u && lit2 && op == isize) ? 2u : ex;
-  const bool emit2 = ex == 0u && lit2;
-  sink.literal_if(emit2, op, sym2);
-  op += emit2 ? 1u : 0u;
-  const uint32_t m = emit1 ? sym2 : sym1;
-  const bool ism = ex == 0u && !emit2 && !lit2;
-  ex = (ism && m == 256u) ? 1u : ex;
-  ex = (ism && m > 285u) ? 3u : ex;
-  const bool dom = ism && m > 256u && m <= 285u;
-  uint32_t lbase, lext;
-  length_base(dom ? m : 257u, lbase, lext);
-  ein_refill(in);
-  lext = dom ? lext : 0u;
-  const uint32_t mlen = lbase + ein_peek(in, lext);
-  ein_drop(in, lext);
-  uint32_t dh;
-  const bool okd = huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh);
-  const uint32_t dsym = syms_d[okd ? idx : 0u];
-  ex = (dom && !okd) ? 3u : ex;
-  ein_drop(in, (dom && okd) ? L : 0u);
-  ex = (dom && okd && dsym > 29u) ? 3u : ex;
-  const bool dom2 = dom && ex == 0u;
-  uint32_t dbase, dext;
-  dist_base(dom2 ? dsym : 0u, dbase, dext);
-  dext = dom2 ? dext : 0u;
-  const uint32_t dist = dbase + ein_peek(in, dext);
-  ein_drop(in, dext);
-  ex = (dom2 && op == isize) ? 2u : ex;
-  ex = (dom2 && ex == 0u && dist > op) ? 3u : ex;
-  const bool domatch = dom2 && ex == 0u;
-  uint32_t n = isize - op;
-  n = mlen < n ? mlen : n;
-  sink.match_if(domatch, op, n, dist);
-  op += domatch ? n : 0u;
-  ex = (domatch && n < mlen) ? 2u : ex;
-  return ex;
-}
-#if HBAM_TOK_SPEC
-// tok_fast_pred with the decode and the output separated: both lit/len lookups run before
-// either symbol read (the second on the bits after the first code, whether or not it turns
-// out to be used), so the two LDS reads are in flight together; the iteration's bytes (up to
-// two literals and a match descriptor, contiguous) then go to the sink as one packet: one
-// chunk-switch test and one spill test per iteration instead of one of each per token.
-// Same outcomes and precedence as tok_fast_pred.
 __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, const HuffP& hd,
                                                   const uint8_t* __restrict__ syms_ll,
                                                   const uint8_t* __restrict__ syms_d, TSink& sink,
@@ -742,8 +574,6 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   ex = (domatch && n < mlen) ? 2u : ex;
   return ex;
 }
-#endif
-#endif
 // One symbol with every zlib outcome checked (the stream's last 64 bits).
 __device__ __forceinline__ uint32_t tok_careful(EIn& in, const HuffP& hl, const HuffP& hd,
                                                 const uint8_t* __restrict__ syms_ll,
@@ -957,13 +787,7 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
         if ((__builtin_amdgcn_readfirstlane(++it) & (TOK_K - 1u)) == 0u) ein_epoch(in);
         if (!ein_short(in, TOK_FAST_BITS)) {  // else stall until the next epoch merges more input
           if (in.total - in.consumed >= TOK_FAST_BITS)
-#if HBAM_TOK_PRED && HBAM_TOK_SPEC
             ex = tok_fast_spec(in, hl, hd, syms_ll, syms_d, sink, op, isize);
-#elif HBAM_TOK_PRED
-            ex = tok_fast_pred(in, hl, hd, syms_ll, syms_d, sink, op, isize);
-#else
-            ex = tok_fast(in, hl, hd, syms_ll, syms_d, sink, op, isize);
-#endif
           else
             ex = tok_careful(in, hl, hd, syms_ll, syms_d, sink, op, isize);
         }

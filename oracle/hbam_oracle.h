@@ -33,8 +33,8 @@ enum {
   OR_EREFID = -6,     /* IllegalArgumentException (reference index not in dictionary) */
   OR_EDATA = -7,      /* RuntimeException wrapping java.util.zip.DataFormatException */
   OR_ENOMEM = -8,     /* host allocation failure (never modelled as OOM) */
-  OR_ETRIBBLE = -9,   /* htsjdk TribbleException (BCF2Codec) */
-  OR_ERUNTIME = -10   /* another RuntimeException escaping BCF2Codec.decode (unpinned) */
+  OR_ETRIBBLE = -14,  /* htsjdk TribbleException (BCF2Codec); = HBAM_ETRIBBLE */
+  OR_ERUNTIME = -15   /* another RuntimeException escaping BCF2Codec.decode (unpinned); = HBAM_ERUNTIME */
 };
 
 /* MurmurHash3.murmurhash3(byte[], int) — util/MurmurHash3.java:32-102 */

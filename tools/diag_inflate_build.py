@@ -26,6 +26,8 @@ ap.add_argument("--seed", type=int, default=3)
 ap.add_argument("--libs", nargs="+", default=["libhbam.so"])
 ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "diag"))
 ap.add_argument("--keep", type=int, default=6, help="bad blocks saved per library")
+ap.add_argument("--variants", nargs="+", default=["att:0"],
+                help="att|noatt:FIRST - attach the profile buffer or not; inflate blocks FIRST.. only")
 a = ap.parse_args()
 os.makedirs(a.out, exist_ok=True)
 torch.cuda.init()
@@ -35,15 +37,17 @@ d[:len(data)].copy_(torch.from_numpy(data))
 d[len(data):].zero_()
 torch.cuda.synchronize()
 summary = {}
-for lib in a.libs:
+for lib, var in [(x, v) for x in a.libs for v in a.variants]:
+    attach, first = var.split(":")[0] == "att", int(var.split(":")[1])
     _lib._LIB = None
     L = _lib.load(os.path.join(ROOT, "hadoop-bam_amd", lib))
     ctx = _lib.Context(0)
     rc, blocks = ctx.scan_blocks(d[:len(data)])
     assert rc == 0, rc
+    blocks = {k: v[first:] for k, v in blocks.items()}
     n = len(blocks["coff"])
     prof = None
-    if hasattr(L, "hbam_prof_attach"):
+    if attach and hasattr(L, "hbam_prof_attach"):
         prof = torch.zeros(32 * n, dtype=torch.int64, device="cuda")
         L.hbam_prof_attach.argtypes = [C.c_void_p]
         assert L.hbam_prof_attach(C.c_void_p(prof.data_ptr())) == 0
@@ -57,7 +61,7 @@ for lib in a.libs:
                         off.ctypes.data, st.ctypes.data)
     torch.cuda.synchronize()
     bad = np.nonzero(st != 0)[0]
-    rec = {"rc": int(rc), "blocks": n, "bad": int(len(bad)), "status_hist": {}, "first": []}
+    rec = {"variant": var, "first_block": first, "rc": int(rc), "blocks": n, "bad": int(len(bad)), "status_hist": {}, "first": []}
     for s in np.unique(st[bad]):
         rec["status_hist"][int(s)] = int(np.sum(st[bad] == s))
     if prof is not None:
@@ -66,7 +70,7 @@ for lib in a.libs:
             L.hbam_prof_attach(C.c_void_p(0))
     for b in bad[:a.keep]:
         b = int(b)
-        e = {"block": b, "status": int(st[b]), "coff": int(blocks["coff"][b]), "clen": int(blocks["clen"][b]),
+        e = {"block": b + first, "launch_index": b, "status": int(st[b]), "coff": int(blocks["coff"][b]), "clen": int(blocks["clen"][b]),
              "isize": int(blocks["isize"][b])}
         if prof is not None:
             e.update(produced=int(P[b, 11]), iters=int(P[b, 24]), consumed=int(P[b, 25]),
@@ -74,11 +78,11 @@ for lib in a.libs:
                      it=int(P[b, 27]))
         c0 = int(blocks["coff"][b])
         raw = bytes(data[c0:c0 + int(blocks["clen"][b])])
-        with open(os.path.join(a.out, "%s_blk%d.bgzf" % (lib, b)), "wb") as f:
+        with open(os.path.join(a.out, "%s_blk%d.bgzf" % (lib, b + first)), "wb") as f:
             f.write(raw)
         rec["first"].append(e)
-    summary[lib] = rec
-    print(lib, json.dumps(rec), flush=True)
+    summary[lib + " " + var] = rec
+    print(lib, var, json.dumps(rec), flush=True)
     ctx.close()
 with open(os.path.join(a.out, "summary.json"), "w") as f:
     json.dump(summary, f, indent=1)
