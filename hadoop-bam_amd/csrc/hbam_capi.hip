@@ -331,8 +331,25 @@ int build_chain(hbam_ctx* c, const uint8_t* dcomp, uint64_t comp_len, uint64_t s
   HIPCHK(c, hipMemcpyAsync(c->pinned_small, small, 16, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const uint32_t ovf = ((uint32_t*)c->pinned_small)[0];
-  const uint32_t bad = ((uint32_t*)c->pinned_small)[1];
-  if (ovf) return set_err(c, HBAM_EUNSUPPORTED, "too many BGZF magic candidates per chunk");
+  uint32_t bad = ((uint32_t*)c->pinned_small)[1];
+  if (ovf) {
+    // more than SCAN_CAP candidates in some chunk (blocks of < 1 KiB compressed, or data full
+    // of magic patterns): the exact two-pass scan writes the whole candidate list
+    k_scan_count<<<(uint32_t)nchunks, 256, 0, c->stream>>>(dcomp, start, comp_len, chunk_cnt);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = scan_exclusive<uint32_t>(c, chunk_cnt, nchunks, chunk_base, &ncand))) return rc;
+    if ((rc = ensure(c, B_CAND, ncand + 1, &cand))) return rc;
+    if ((rc = ensure(c, B_BLK, ncand + 1, &blk))) return rc;
+    HIPCHK(c, hipMemsetAsync(small, 0, 16 * 8, c->stream));
+    k_scan_write<<<(uint32_t)nchunks, 256, 0, c->stream>>>(dcomp, start, comp_len, chunk_base, cand);
+    if (ncand)
+      k_verify_chain<<<grid_for(ncand, 256), 256, 0, c->stream>>>(dcomp, cand, ncand, comp_len,
+                                                                   blk, nbad);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->pinned_small, small, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    bad = ((uint32_t*)c->pinned_small)[1];
+  }
   // download candidate list only if the fast path failed or to check the ends
   uint64_t first = ~0ULL;
   BlockRec last{};

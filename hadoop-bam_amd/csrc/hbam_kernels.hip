@@ -39,6 +39,26 @@ static __device__ __forceinline__ uint16_t ld_u16_unaligned(const uint8_t* p) { 
 // length is BSIZE (u16 @16) + 1.  One workgroup scans a SCAN_CHUNK-byte chunk; candidates
 // are collected in LDS, sorted, and written to a per-chunk slot (cap SCAN_CAP).
 // ------------------------------------------------------------------------------------
+// Candidate test of the 16 positions [p0, p0 + 16): bit k set when p0 + k can start a block.
+__device__ __forceinline__ uint32_t scan_mask16(const uint8_t* __restrict__ comp, uint64_t p0, uint64_t end) {
+  uint32_t w[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
+  uint32_t mask = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t p = p0 + k;
+    // bytes p..p+3 and p+10..p+11
+    const int q = k >> 2, r = k & 3;
+    const uint64_t lo = (uint64_t)w[q] | (uint64_t)w[q + 1] << 32;
+    const uint32_t m = (uint32_t)(lo >> (8 * r));
+    const uint64_t lo2 = (uint64_t)w[(k + 8) >> 2] | (uint64_t)w[((k + 8) >> 2) + 1] << 32;
+    const uint32_t x = (uint32_t)(lo2 >> (8 * ((k + 8) & 3)));  // bytes p+8..p+11
+    if (p + 18 <= end && m == 0x04088b1fu && (x >> 16) == 6u) mask |= 1u << k;
+  }
+  return mask;
+}
+
 __global__ __launch_bounds__(256) void k_scan_chunks(const uint8_t* __restrict__ comp,
                                                      uint64_t begin, uint64_t end,
                                                      uint32_t* __restrict__ chunk_cnt,
@@ -50,29 +70,16 @@ __global__ __launch_bounds__(256) void k_scan_chunks(const uint8_t* __restrict__
   const uint64_t c0 = begin + chunk * SCAN_CHUNK;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
-  // each thread tests 16 consecutive positions per step using a 32-byte window
+  // each thread tests 16 consecutive positions per step using a 36-byte window
   for (uint32_t step = 0; step < SCAN_CHUNK / (256 * 16); ++step) {
     const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * 16;
     if (p0 >= end) break;
-    // 16-byte aligned relative to comp (begin is 16-aligned by construction of callers? no:
-    // use byte loads for the window to stay alignment-agnostic)
-    uint32_t w[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint64_t p = p0 + k;
-      if (p + 18 > end) break;
-      // bytes p..p+3 and p+10..p+11
-      const int q = k >> 2, r = k & 3;
-      const uint64_t lo = (uint64_t)w[q] | (uint64_t)w[q + 1] << 32;
-      const uint32_t m = (uint32_t)(lo >> (8 * r));
-      const uint64_t lo2 = (uint64_t)w[(k + 8) >> 2] | (uint64_t)w[((k + 8) >> 2) + 1] << 32;
-      const uint32_t x = (uint32_t)(lo2 >> (8 * ((k + 8) & 3)));  // bytes p+8..p+11
-      if (m == 0x04088b1fu && (x >> 16) == 6u) {
-        const uint32_t i = atomicAdd(&s_cnt, 1u);
-        if (i < SCAN_CAP) s_pos[i] = p;
-      }
+    uint32_t mask = scan_mask16(comp, p0, end);
+    while (mask) {
+      const uint32_t k = __ffs(mask) - 1u;
+      mask &= mask - 1u;
+      const uint32_t i = atomicAdd(&s_cnt, 1u);
+      if (i < SCAN_CAP) s_pos[i] = p0 + k;
     }
   }
   __syncthreads();
@@ -91,6 +98,63 @@ __global__ __launch_bounds__(256) void k_scan_chunks(const uint8_t* __restrict__
     }
     chunk_cnt[chunk] = n;
     for (uint32_t i = 0; i < n; ++i) chunk_pos[chunk * SCAN_CAP + i] = s_pos[i];
+  }
+}
+
+// Exact two-pass form of the candidate scan, for files whose blocks are so small (or whose
+// data holds so many magic patterns) that a chunk has more than SCAN_CAP candidates: pass 1
+// counts each chunk's candidates, pass 2 writes them at the chunk's exclusive-scan offset in
+// position order (a workgroup scan of the per-thread counts at every step), straight into
+// the candidate list.
+__global__ __launch_bounds__(256) void k_scan_count(const uint8_t* __restrict__ comp, uint64_t begin,
+                                                    uint64_t end, uint32_t* __restrict__ chunk_cnt) {
+  __shared__ uint32_t s_cnt;
+  const uint64_t c0 = begin + (uint64_t)blockIdx.x * SCAN_CHUNK;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  uint32_t n = 0;
+  for (uint32_t step = 0; step < SCAN_CHUNK / (256 * 16); ++step) {
+    const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * 16;
+    if (p0 >= end) break;
+    n += __popc(scan_mask16(comp, p0, end));
+  }
+  atomicAdd(&s_cnt, n);
+  __syncthreads();
+  if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = s_cnt;
+}
+__global__ __launch_bounds__(256) void k_scan_write(const uint8_t* __restrict__ comp, uint64_t begin,
+                                                    uint64_t end, const uint64_t* __restrict__ chunk_base,
+                                                    uint64_t* __restrict__ cand) {
+  __shared__ uint32_t s_wsum[4];
+  const uint64_t c0 = begin + (uint64_t)blockIdx.x * SCAN_CHUNK;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint64_t run = chunk_base[blockIdx.x];
+  for (uint32_t step = 0; step < SCAN_CHUNK / (256 * 16); ++step) {
+    const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * 16;
+    uint32_t mask = p0 < end ? scan_mask16(comp, p0, end) : 0u;
+    const uint32_t cnt = __popc(mask);
+    uint32_t incl = cnt;  // inclusive scan within the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = __shfl_up(incl, off);
+      if ((int)lane >= off) incl += t;
+    }
+    if (lane == 63) s_wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      before += j < wv ? s_wsum[j] : 0u;
+      total += s_wsum[j];
+    }
+    uint64_t o = run + before + incl - cnt;
+    while (mask) {
+      const uint32_t k = __ffs(mask) - 1u;
+      mask &= mask - 1u;
+      cand[o++] = p0 + k;
+    }
+    run += total;
+    __syncthreads();
   }
 }
 
@@ -181,8 +245,15 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
 #ifdef HBAM_PROF
     uint64_t pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pc[4] = {0, 0, 0, 0};
 #endif
-    st = inflate_tokens_block(comp + r.coff + 18, r.clen - 26u, r.isize, s_ll + threadIdx.x * 288,
-                              s_d + threadIdx.x * 32, lens_scratch + (uint64_t)b * LENS_SLOT, sink,
+#if HBAM_TOK_ILV
+    uint8_t* const my_ll = s_ll + 4u * threadIdx.x;  // interleaved (sym_at): 72 rows of 256 B
+    uint8_t* const my_d = s_d + 4u * threadIdx.x;    //                        8 rows of 256 B
+#else
+    uint8_t* const my_ll = s_ll + threadIdx.x * 288;
+    uint8_t* const my_d = s_d + threadIdx.x * 32;
+#endif
+    st = inflate_tokens_block(comp + r.coff + 18, r.clen - 26u, r.isize, my_ll, my_d,
+                              lens_scratch + (uint64_t)b * LENS_SLOT, sink,
                               &produced
 #ifdef HBAM_PROF
                               , pt, pc

@@ -87,6 +87,37 @@ def test_thousands_of_empty_blocks(gpu_ctx, oracle_mod, genbam):
         assert_same_split(got, ref)
 
 
+@pytest.mark.parametrize("kw", [dict(payload=64, level=6), dict(payload=300, level=1, straddle=0),
+                                dict(records=20000, empty_every=1, payload=200, level=9)])
+def test_tiny_blocks_scan_and_decode(gpu_ctx, oracle_mod, genbam, kw):
+    """BGZF blocks far below 1 KiB compressed (more than the block scan's 64 candidate slots per
+    64 KiB chunk: the exact two-pass scan takes over): the block table, the whole-file read
+    and every guessed split equal the oracle's."""
+    kw = dict(kw)
+    m = np.asarray(genbam.generate(records=kw.pop("records", 3000), seed=35, **kw))
+    ref_b = oracle_mod.scan_blocks(m)
+    assert len(ref_b["coff"]) > 64 * (len(m) // 65536 + 1)  # some chunk overflows
+    rc, blocks = gpu_ctx.scan_blocks(m)
+    assert rc == 0, gpu_ctx.last_error()
+    for k in ("coff", "clen", "isize", "crc"):
+        assert np.array_equal(blocks[k], ref_b[k]), k
+    h = oracle_mod.read_header(m)
+    ref = oracle_mod.read_split(m, h["first_voffset"], _whole(m))
+    got = gpu_ctx.decode_split(m, h["first_voffset"], _whole(m), n_ref=-1)
+    assert got["rc"] == 0, got
+    assert_same_split(got, ref)
+    b, e = oracle_mod.file_splits(len(m), 1 << 17)
+    want = oracle_mod.probabilistic_splits(m, b, e)
+    n, vs, ve = gpu_ctx.probabilistic_splits(m, b, e)
+    assert not isinstance(want, int) and n == len(want[0])
+    assert np.array_equal(vs, want[0]) and np.array_equal(ve, want[1])
+    for a, z in zip(vs, ve):
+        ref = oracle_mod.read_split(m, int(a), int(z))
+        got = gpu_ctx.decode_split(m, int(a), int(z), n_ref=h["n_ref"])
+        assert got["rc"] == 0, got
+        assert_same_split(got, ref)
+
+
 def _bgzf_block(payload, level=6):
     """One BGZF block (BSIZE/CRC/ISIZE as htsjdk writes them) holding `payload`."""
     import struct
@@ -122,6 +153,43 @@ def test_inflate_every_output_misalignment(gpu_ctx, fname):
         assert rc == 0 and np.all(st == 0), (lead, st)
         for j, b in enumerate(lst[1 if lead else 0:], start=1 if lead else 0):
             assert u[int(off[j]):int(off[j + 1])].tobytes() == want[b[0]], (lead, j)
+
+
+def test_inflate_independent_of_launch_position(gpu_ctx, oracle_mod, genbam):
+    """The r02 profiling-build failure depended on a block's position in the
+    launch, not on its bytes: only waves that started in a slot an earlier wave of the launch
+    had vacated decoded wrongly.  Here the same blocks (zlib levels 1/5/9, uniform and binned
+    qualities, stored and fixed-Huffman blocks) are repeated until the launch holds ~2.7
+    waves per slot of the whole chip (2 waves/SIMD x 4 SIMDs x 256 CUs), so most copies run in a
+    reused slot; every copy must inflate CRC-clean on the device (status 0)."""
+    import ctypes as C
+    from hadoop_bam import _lib
+    parts = [np.asarray(genbam.generate(records=4000, seed=31, level=1)),
+             np.asarray(genbam.generate(records=4000, seed=32, level=9, uniform_qual=1)),
+             np.asarray(genbam.generate(records=1500, seed=33, level=0)),
+             np.asarray(genbam.generate(records=1500, seed=34, payload=64, level=6))]
+    base, coffs, clens, isz, crcs = 0, [], [], [], []
+    for d in parts:
+        b = oracle_mod.scan_blocks(d)  # the block list only (this test is about the inflate)
+        if len(b["coff"]) > 100:  # the fixed-Huffman file: a sample of its 64-byte blocks
+            b = {k: v[:100] for k, v in b.items()}
+        coffs += [int(c) + base for c in b["coff"]]
+        clens += list(b["clen"]); isz += list(b["isize"]); crcs += list(b["crc"])
+        base += len(d)
+    data = np.concatenate(parts)
+    nuniq = len(coffs)
+    n = -(-350_000 // nuniq) * nuniq  # ~2.7 x 131,072 resident lanes
+    arr = (_lib.Block * n)()
+    for i in range(n):
+        j = i % nuniq
+        arr[i].coff, arr[i].clen, arr[i].isize, arr[i].crc = coffs[j], int(clens[j]), int(isz[j]), int(crcs[j])
+    off = np.zeros(n + 1, np.uint64)
+    st = np.full(n, 99, np.int32)
+    rc = gpu_ctx.L.hbam_inflate(gpu_ctx.h, C.c_void_p(data.ctypes.data), 0, len(data), arr, n, 1,
+                                None, 0, off.ctypes.data, st.ctypes.data)
+    assert rc == 0, gpu_ctx.last_error()
+    bad = np.nonzero(st != 0)[0]
+    assert len(bad) == 0, (len(bad), n, bad[:8], st[bad[:8]])
 
 
 @pytest.mark.parametrize("kw", [dict(level=0), dict(level=1), dict(level=9),
