@@ -245,13 +245,11 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
 #ifdef HBAM_PROF
     uint64_t pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pc[4] = {0, 0, 0, 0};
 #endif
-#if HBAM_TOK_ILV
-    uint8_t* const my_ll = s_ll + 4u * threadIdx.x;  // interleaved (sym_at): 72 rows of 256 B
-    uint8_t* const my_d = s_d + 4u * threadIdx.x;    //                        8 rows of 256 B
-#else
+    // per-lane symbol tables, lane-contiguous (dword-interleaving them across the lanes removes
+    // the LDS bank conflicts, 75 % of the pass's LDS cycles, but not time: 33.7 vs 34.3 ms at
+    // 5 GB, profiles/r03/ab/huffman_interleaved_symtab_5g.txt)
     uint8_t* const my_ll = s_ll + threadIdx.x * 288;
     uint8_t* const my_d = s_d + threadIdx.x * 32;
-#endif
     st = inflate_tokens_block(comp + r.coff + 18, r.clen - 26u, r.isize, my_ll, my_d,
                               lens_scratch + (uint64_t)b * LENS_SLOT, sink,
                               &produced

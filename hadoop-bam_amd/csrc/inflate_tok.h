@@ -59,22 +59,6 @@ constexpr uint32_t TOK_K = HBAM_TOK_K;
 // stream bits one fast-path iteration may consume: 2 lit/len codes + length extra + distance
 // code + distance extra = 15+15+5+15+13 = 63 (<= 64)
 constexpr uint32_t TOK_FAST_BITS = 64u;
-#ifndef HBAM_TOK_ILV
-#define HBAM_TOK_ILV 0  // A/B: symbol tables interleaved across the lanes by dword
-#endif
-// Symbol-table layout in LDS.  Lane-contiguous (ILV 0): entry j of a lane at its base + j, the
-// lanes' bases 288 B apart.  Interleaved (ILV 1): the tables of the workgroup's 64 lanes are
-// dword-interleaved, entry j of a lane at its base (lane * 4) + (j / 4) * 256 + j % 4, so a
-// wave's 64 reads of one entry index fall in 64 different dwords / banks whatever the index
-// (the SQ counters show 75 % of the pass's LDS cycles as bank conflicts with the contiguous
-// layout: profiles/r03/evidence/pmc_sq_2g.json).
-__device__ __forceinline__ uint32_t sym_at(uint32_t j) {
-#if HBAM_TOK_ILV
-  return (j >> 2) * 256u + (j & 3u);
-#else
-  return j;
-#endif
-}
 constexpr uint32_t TOK_LENS_LL = 32;    // lens scratch: lit/len code lengths at +32 ..
 constexpr uint32_t TOK_LENS_D = 320;    //               distance code lengths at +320 (<= 30)
 
@@ -504,7 +488,7 @@ __device__ __attribute__((noinline)) bool tok_build(const uint8_t* __restrict__ 
           pos = eq ? next[L] : pos;
           next[L] += eq ? 1u : 0u;
         }
-        syms[sym_at(pos)] = (SymT)s;
+        syms[pos] = (SymT)s;
       }
     }
   }
@@ -532,8 +516,8 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   const uint32_t l1 = ok1 ? L1 : 0u;
   const uint32_t v2 = __builtin_bitreverse32((uint32_t)(in.bb >> l1)) >> 17;
   const bool ok2 = huffp_lookup<true>(hl, v2, L2, idx2, hi2);
-  const uint32_t sym1 = (uint32_t)syms_ll[sym_at(ok1 ? idx1 : 0u)] | hi1;
-  const uint32_t sym2 = (uint32_t)syms_ll[sym_at(ok2 ? idx2 : 0u)] | hi2;
+  const uint32_t sym1 = (uint32_t)syms_ll[ok1 ? idx1 : 0u] | hi1;
+  const uint32_t sym2 = (uint32_t)syms_ll[ok2 ? idx2 : 0u] | hi2;
   uint32_t ex = ok1 ? 0u : 3u;
   ein_drop(in, l1);
   const bool lit1 = ok1 && sym1 < 256u;
@@ -560,7 +544,7 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   ein_drop(in, lext);
   uint32_t L, idx, dh;
   const bool okd = huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh);
-  const uint32_t dsym = syms_d[sym_at(okd ? idx : 0u)];
+  const uint32_t dsym = syms_d[okd ? idx : 0u];
   ex = (dom && !okd) ? 3u : ex;
   ein_drop(in, (dom && okd) ? L : 0u);
   ex = (dom && okd && dsym > 29u) ? 3u : ex;
@@ -599,7 +583,7 @@ __device__ __forceinline__ uint32_t tok_careful(EIn& in, const HuffP& hl, const 
   uint32_t L, idx, hi = 0;
   if (!huffp_lookup<true>(hl, ein_rev15(in), L, idx, hi)) return ein_avail(in) >= 1u ? 3u : 2u;
   if (L > ein_avail(in)) return 2u;
-  const uint32_t sym = (uint32_t)syms_ll[sym_at(idx)] | hi;
+  const uint32_t sym = (uint32_t)syms_ll[idx] | hi;
   ein_drop(in, L);
   if (sym < 256u) {
     if (op == isize) return 2u;
@@ -617,7 +601,7 @@ __device__ __forceinline__ uint32_t tok_careful(EIn& in, const HuffP& hl, const 
   uint32_t dh;
   if (!huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh)) return ein_avail(in) >= 1u ? 3u : 2u;
   if (L > ein_avail(in)) return 2u;
-  const uint32_t dsym = syms_d[sym_at(idx)];
+  const uint32_t dsym = syms_d[idx];
   ein_drop(in, L);
   if (dsym > 29u) return 3u;
   uint32_t dbase, dext;
@@ -744,7 +728,7 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
             const uint32_t v = ein_rev15(in);
             huff_lookup(hc, v, L, idx);  // CODES sets are complete
             if (L > ein_avail(in)) goto leave;
-            sym = syms_ll[sym_at(idx)];
+            sym = syms_ll[idx];
           }
           if (sym < 16u) {
             ein_drop(in, L);
