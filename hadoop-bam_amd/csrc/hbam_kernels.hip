@@ -32,6 +32,9 @@ typedef uint32_t u32_a1 __attribute__((aligned(1)));
 typedef uint16_t u16_a1 __attribute__((aligned(1)));
 static __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) { return *(const u32_a1*)p; }
 static __device__ __forceinline__ uint16_t ld_u16_unaligned(const uint8_t* p) { return *(const u16_a1*)p; }
+// 16 bytes at any byte address as one global_load_dwordx4
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+static __device__ __forceinline__ u32x4_a1 ld_16_unaligned(const uint8_t* p) { return *(const u32x4_a1*)p; }
 
 // ------------------------------------------------------------------------------------
 // K1: candidate BGZF block starts.  htsjdk accepts a block when bytes 0..3 = 1f 8b 08 04
@@ -41,9 +44,10 @@ static __device__ __forceinline__ uint16_t ld_u16_unaligned(const uint8_t* p) { 
 // ------------------------------------------------------------------------------------
 // Candidate test of the 16 positions [p0, p0 + 16): bit k set when p0 + k can start a block.
 __device__ __forceinline__ uint32_t scan_mask16(const uint8_t* __restrict__ comp, uint64_t p0, uint64_t end) {
-  uint32_t w[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
+  // bytes p0 .. p0+35 as three 16-byte loads (nine dword loads before: 3.0 ms per 10 GB)
+  const u32x4_a1 q0 = ld_16_unaligned(comp + p0), q1 = ld_16_unaligned(comp + p0 + 16);
+  const uint32_t w8 = ld_u32_unaligned(comp + p0 + 32);
+  const uint32_t w[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], w8};
   uint32_t mask = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -932,18 +936,21 @@ __global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,
   uint8_t lrn = 0, mapq = 0;
   uint16_t bin = 0, ncig = 0, flag = 0;
   if (st == ST_OK) {
+    // the fixed part (bytes 4..35) as two 16-byte loads and one dword
     const uint8_t* p = u + r;
-    ref = (int32_t)ld_u32_unaligned(p + 4);
-    pos = (int32_t)ld_u32_unaligned(p + 8);
-    lrn = p[12];
-    mapq = p[13];
-    bin = ld_u16_unaligned(p + 14);
-    ncig = ld_u16_unaligned(p + 16);
-    flag = ld_u16_unaligned(p + 18);
-    lseq = (int32_t)ld_u32_unaligned(p + 20);
-    nref = (int32_t)ld_u32_unaligned(p + 24);
-    npos = (int32_t)ld_u32_unaligned(p + 28);
-    tlen = (int32_t)ld_u32_unaligned(p + 32);
+    const u32x4_a1 f0 = ld_16_unaligned(p + 4), f1 = ld_16_unaligned(p + 20);
+    const uint32_t f2 = ld_u32_unaligned(p + 32);
+    ref = (int32_t)f0[0];
+    pos = (int32_t)f0[1];
+    lrn = (uint8_t)f0[2];
+    mapq = (uint8_t)(f0[2] >> 8);
+    bin = (uint16_t)(f0[2] >> 16);
+    ncig = (uint16_t)f0[3];
+    flag = (uint16_t)(f0[3] >> 16);
+    lseq = (int32_t)f1[0];
+    nref = (int32_t)f1[1];
+    npos = (int32_t)f1[2];
+    tlen = (int32_t)f2;
     if (validate_refs && ((ref != -1 && (ref < 0 || ref >= n_ref)) ||
                           (nref != -1 && (nref < 0 || nref >= n_ref))))
       st = HBAM_EREFID;

@@ -19,7 +19,8 @@ import numpy as np  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=float, default=20e9)
-    ap.add_argument("--window", type=float, default=4e9)
+    ap.add_argument("--window", type=float, nargs="+", default=[4e9],
+                    help="window sizes (compressed bytes); one JSON line each")
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--reps", type=int, default=2)
     a = ap.parse_args()
@@ -46,31 +47,41 @@ def main():
     rc, blocks = ctx.scan_blocks(host[:n])
     assert rc == 0
     U = int(np.sum(blocks["isize"].astype(np.uint64)))  # the file's inflated bytes
+    for win in a.window:
+        one_window_size(a, ctx, host, n, nrec, h, v0, v1, U, int(win))
+
+
+def one_window_size(a, ctx, host, n, nrec, h, v0, v1, U, win):
+    import torch
     reps = []
     for r in range(a.reps):
         torch.cuda.synchronize()
         t0 = time.time()
         recs, ub, wins = 0, 0, 0
-        keysum = 0
-        for d in ctx.split_stream(host[:n], v0, v1, h["n_ref"], window_bytes=int(a.window), host=False):
+        marks = []
+        for d in ctx.split_stream(host[:n], v0, v1, h["n_ref"], window_bytes=win, host=False):
             recs += int(d.n_records)
             wins += 1
             if int(d.status) != 0:
                 raise RuntimeError("window status %d" % d.status)
-            ub += int(ctx.timing()["ubuf_bytes"])  # per window, overlap re-reads included
+            t = ctx.timing()
+            ub += int(t["ubuf_bytes"])  # per window, overlap re-reads included
+            marks.append((round(time.time() - t0, 4), round(t["total_ms"], 2)))
         dt = time.time() - t0
         st = ctx.last_stream_stats
-        reps.append((dt, recs, ub, wins, st))
-        print("rep %d: %.3fs %d records %d windows h2d %.1f GB in %.1f ms" % (
-            r, dt, recs, wins, st["h2d_bytes"] / 1e9, st["h2d_ms"]), file=sys.stderr, flush=True)
-    dt, recs, ub, wins, st = min(reps, key=lambda x: x[0])
+        reps.append((dt, recs, ub, wins, st, marks))
+        print("window %.1f GB rep %d: %.3fs %d records %d windows h2d %.1f GB in %.1f ms; per window "
+              "(host s at return, decode ms): %s" % (win / 1e9, r, dt, recs, wins, st["h2d_bytes"] / 1e9,
+                                                     st["h2d_ms"], marks), file=sys.stderr, flush=True)
+    dt, recs, ub, wins, st, marks = min(reps, key=lambda x: x[0])
     ok = recs == nrec
     print(json.dumps({
         "metric": "streamed split decode, PCIe-inclusive (config#4 shape, one MI355X)",
         "value": round(U / dt / 1e9, 3), "unit": "GB/s uncompressed", "uncompressed_bytes": U,
         "inflated_incl_window_overlap": ub, "records_per_s": round(recs / dt, 1),
         "compressed_gb_s": round(n / dt / 1e9, 3), "seconds": round(dt, 4), "all_reps_s": [round(x[0], 4) for x in reps],
-        "file_bytes": n, "window_bytes": int(a.window), "windows": wins, "records": recs,
+        "file_bytes": n, "window_bytes": win, "windows": wins, "records": recs,
+        "per_window_host_s_and_decode_ms": marks,
         "h2d": {"bytes": st["h2d_bytes"], "ms": round(st["h2d_ms"], 2),
                 "gb_s": round(st["h2d_bytes"] / max(st["h2d_ms"], 1e-9) / 1e6, 2)},
         "host_buffer": "page-locked for libhbam (hbam_host_register)", "record_count_matches_generator": ok}), flush=True)
