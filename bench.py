@@ -128,9 +128,30 @@ def cpu_baseline(data, budget_s, threads):
                       % (sample / 1e9, rec, ub / 1e9, len(vs))}
 
 
-def parity_at_size(ctx, buf, dbuf, n_splits, seed, threads):
+POOLS = (("names", "name_off"), ("cigars", "cigar_off"), ("seq", "seq_off"), ("qual", "seq_off"),
+         ("aux", "aux_off"))
+
+
+def same_records(a, i0, b, j0, n):
+    """records [i0, i0+n) of host columns a == records [j0, j0+n) of b: every fixed column and
+    every decoded field pool (names, CIGAR, SEQ, QUAL, AUX)"""
+    for k in ("voffset", "key", "block_size", "ref_id", "pos", "flag", "l_seq", "tlen", "mapq",
+              "bin", "n_cigar", "l_read_name", "next_ref_id", "next_pos", "layout_ok"):
+        if not np.array_equal(a[k][i0:i0 + n], b[k][j0:j0 + n]):
+            return False
+    for pool, off in POOLS:
+        x = a[pool][int(a[off][i0]):int(a[off][i0 + n])]
+        y = b[pool][int(b[off][j0]):int(b[off][j0 + n])]
+        if not np.array_equal(x, y):
+            return False
+    return True
+
+
+def parity_at_size(ctx, buf, dbuf, n_splits, seed, threads, whole=None):
     """n_splits random 32 MiB Hadoop FileSplits inside the rank's range: guess + decode on the
-    device vs guess + BAMRecordReader of the oracle, every column and every record byte."""
+    device vs guess + BAMRecordReader of the oracle, every column, every decoded field pool and
+    every record byte; then the same records inside the timed whole-shard decode (`whole`, its
+    host copy) against the split's verified decode, so the big launch itself is checked."""
     import oracle
     rng = np.random.default_rng(seed)
     span = len(buf) - (48 << 20)
@@ -142,6 +163,7 @@ def parity_at_size(ctx, buf, dbuf, n_splits, seed, threads):
     assert rc == 0
     sub = np.ascontiguousarray(buf)
     mism, recs = 0, 0
+    w_recs, w_max, w_mism = 0, 0, 0
     res = [None] * n_splits
 
     def ref_one(i):
@@ -173,10 +195,26 @@ def parity_at_size(ctx, buf, dbuf, n_splits, seed, threads):
         if same:
             pay, _ = oracle.record_payloads(r)
             same = d["ubuf"].tobytes() == pay.tobytes()
+        if same:
+            op = oracle.pools(r)
+            same = np.array_equal(d["layout_ok"], op["layout_ok"]) and all(
+                np.array_equal(d[k], op[k]) for k in ("names", "cigars", "seq", "qual", "aux"))
         mism += 0 if same else 1
-    return {"splits": n_splits, "mismatches": mism, "records": recs,
-            "what": "random 32 MiB FileSplits of the benchmarked file: guessed start, every "
-                    "column and every record byte vs the oracle"}
+        if whole is not None and same and d["n"]:
+            lo = int(np.searchsorted(whole["voffset"], d["voffset"][0]))
+            ok = lo + d["n"] <= whole["n"] and same_records(whole, lo, d, 0, d["n"])
+            w_recs += d["n"]
+            w_max = max(w_max, lo + d["n"])
+            w_mism += 0 if ok else 1
+    out = {"splits": n_splits, "mismatches": mism, "records": recs,
+           "what": "random 32 MiB FileSplits of the benchmarked file: guessed start, every "
+                   "column, every decoded field pool and every record byte vs the oracle"}
+    if whole is not None:
+        out["whole_shard"] = {"records_checked": w_recs, "highest_record_index": w_max,
+                              "shard_records": whole["n"], "mismatches": w_mism,
+                              "what": "the same records inside the timed whole-shard decode "
+                                      "(one launch per kernel) equal the verified split decodes"}
+    return out
 
 
 def free_port():
@@ -324,8 +362,17 @@ def main():
     parity = None
     if rank == 0 and args.parity_splits > 0:
         try:
+            # host copy of the timed decode's own output (before any other decode reuses the
+            # context's device buffers)
+            hc = _lib.Columns()
+            rc = ctx.L.hbam_columns_to_host(ctx.h, C.byref(cols), C.byref(hc))
+            if rc:
+                raise RuntimeError("hbam_columns_to_host: %s" % ctx.last_error())
+            whole = _lib.host_columns_to_numpy(hc)
+            ctx.L.hbam_free_host_columns(C.byref(hc))
             parity = parity_at_size(ctx, buf, dcomp[:len(buf)], args.parity_splits, args.seed + 17,
-                                    threads)
+                                    threads, whole=whole)
+            del whole
         except Exception as e:  # reported, never hidden
             parity = {"error": str(e)}
     if rank != 0:

@@ -1118,7 +1118,8 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if ((rc = ensure(c, B_C_AUX, tot_aux + 1, &dc.aux))) return rc;
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   if (n_final)
-    k_decode_pools<<<grid_for(n_final, 4), 256, 0, c->stream>>>(ub, n_final, rec_off, dc);
+    k_decode_pools<<<(uint32_t)std::min<uint64_t>(grid_for(n_final, 256), POOLS_MAX_WG), 256, 0, c->stream>>>(
+        ub, n_final, rec_off, dc);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1909,7 +1910,9 @@ extern "C" int hbam_gather_records(hbam_ctx* c, const uint8_t* ubuf, const uint6
   if (tot > out_cap) return set_err(c, HBAM_EINVAL, "hbam_gather_records: %llu bytes > out_cap %llu",
                                     (unsigned long long)tot, (unsigned long long)out_cap);
   if (n) {
-    const uint64_t g = (n + RS_WG / 64 - 1) / (RS_WG / 64);
+    // one wave per record, grid-stride: a grid of 64 x n threads would pass 2^32 above 67 M
+    // records (the dispatch packet's grid size is 32-bit)
+    const uint64_t g = std::min<uint64_t>((n + RS_WG / 64 - 1) / (RS_WG / 64), GATHER_MAX_WG);
     k_gather_records<<<(uint32_t)g, RS_WG, 0, c->stream>>>(ubuf, rec_off, perm, n, out_off, out);
   }
   HIPCHK(c, hipGetLastError());

@@ -13,6 +13,8 @@ constexpr uint32_t LENS_SLOT = 352;     // per-block global scratch for code len
 constexpr uint32_t BITMAP_WORDS = 2048;  // per-block match-start bitmap (65536 bits)
 constexpr uint32_t WALK_CAP = 1880;     // >= 65536/35 record starts per block (BAM >= 36 B, BCF >= 35 B)
 constexpr uint32_t SCAN_WG = 256;
+constexpr uint32_t POOLS_MAX_WG = 8192;    // k_decode_pools grid cap (grid-stride over records)
+constexpr uint32_t GATHER_MAX_WG = 65536;  // k_gather_records grid cap (grid-stride over records)
 constexpr uint64_t UBUF_SLACK = 8192;  // k_resolve reads whole 2 KiB stretches past a block end
 constexpr uint32_t SCAN_TILE = 4096;
 constexpr uint64_t NO_ENTRY = ~0ULL;

@@ -32,9 +32,6 @@ typedef uint32_t u32_a1 __attribute__((aligned(1)));
 typedef uint16_t u16_a1 __attribute__((aligned(1)));
 static __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t* p) { return *(const u32_a1*)p; }
 static __device__ __forceinline__ uint16_t ld_u16_unaligned(const uint8_t* p) { return *(const u16_a1*)p; }
-// 16 bytes at any byte address as one global_load_dwordx4
-typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
-static __device__ __forceinline__ u32x4_a1 ld_16_unaligned(const uint8_t* p) { return *(const u32x4_a1*)p; }
 
 // ------------------------------------------------------------------------------------
 // K1: candidate BGZF block starts.  htsjdk accepts a block when bytes 0..3 = 1f 8b 08 04
@@ -44,10 +41,10 @@ static __device__ __forceinline__ u32x4_a1 ld_16_unaligned(const uint8_t* p) { r
 // ------------------------------------------------------------------------------------
 // Candidate test of the 16 positions [p0, p0 + 16): bit k set when p0 + k can start a block.
 __device__ __forceinline__ uint32_t scan_mask16(const uint8_t* __restrict__ comp, uint64_t p0, uint64_t end) {
-  // bytes p0 .. p0+35 as three 16-byte loads (nine dword loads before: 3.0 ms per 10 GB)
-  const u32x4_a1 q0 = ld_16_unaligned(comp + p0), q1 = ld_16_unaligned(comp + p0 + 16);
-  const uint32_t w8 = ld_u32_unaligned(comp + p0 + 32);
-  const uint32_t w[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], w8};
+  // (two 16-byte loads instead of the dword loads: 3.07 -> 3.34 ms per 10 GB, not kept)
+  uint32_t w[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
   uint32_t mask = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -936,21 +933,18 @@ __global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,
   uint8_t lrn = 0, mapq = 0;
   uint16_t bin = 0, ncig = 0, flag = 0;
   if (st == ST_OK) {
-    // the fixed part (bytes 4..35) as two 16-byte loads and one dword
     const uint8_t* p = u + r;
-    const u32x4_a1 f0 = ld_16_unaligned(p + 4), f1 = ld_16_unaligned(p + 20);
-    const uint32_t f2 = ld_u32_unaligned(p + 32);
-    ref = (int32_t)f0[0];
-    pos = (int32_t)f0[1];
-    lrn = (uint8_t)f0[2];
-    mapq = (uint8_t)(f0[2] >> 8);
-    bin = (uint16_t)(f0[2] >> 16);
-    ncig = (uint16_t)f0[3];
-    flag = (uint16_t)(f0[3] >> 16);
-    lseq = (int32_t)f1[0];
-    nref = (int32_t)f1[1];
-    npos = (int32_t)f1[2];
-    tlen = (int32_t)f2;
+    ref = (int32_t)ld_u32_unaligned(p + 4);
+    pos = (int32_t)ld_u32_unaligned(p + 8);
+    lrn = p[12];
+    mapq = p[13];
+    bin = ld_u16_unaligned(p + 14);
+    ncig = ld_u16_unaligned(p + 16);
+    flag = ld_u16_unaligned(p + 18);
+    lseq = (int32_t)ld_u32_unaligned(p + 20);
+    nref = (int32_t)ld_u32_unaligned(p + 24);
+    npos = (int32_t)ld_u32_unaligned(p + 28);
+    tlen = (int32_t)ld_u32_unaligned(p + 32);
     if (validate_refs && ((ref != -1 && (ref < 0 || ref >= n_ref)) ||
                           (nref != -1 && (nref < 0 || nref >= n_ref))))
       st = HBAM_EREFID;
@@ -1006,34 +1000,102 @@ __global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,
 }
 
 // Pools: names (l_read_name bytes incl. NUL), CIGAR u32s, SEQ unpacked to
-// "=ACMGRSVTWYHKDBN", QUAL raw, AUX raw.  One wave per record, lanes copy bytes.
+// "=ACMGRSVTWYHKDBN", QUAL raw, AUX raw.  A wave takes a tile of 64 consecutive records (grid-
+// stride over tiles).  Each field's segments are cut into 16-byte units (the last unit of a
+// segment shorter, written in 8/4/2/1-byte pieces, so a neighbour's bytes in the pool are never
+// written); the tile's units are numbered by a wave scan and the lanes take consecutive units,
+// so a wave instruction moves ~1 KiB of consecutive pool bytes from a nearly consecutive source.
+// (r02: one wave per record with byte copies, latency-bound, and a grid of 64 x records threads
+// that passed 2^32 above 67 M records; one thread per record with 16-byte copies: 59.7 ms per
+// 10 GB shard, every store instruction touching 64 lines.)
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint64_t u64_a1 __attribute__((aligned(1)));
+static __device__ __forceinline__ void st_part(uint8_t* d, uint32_t n, u32x4_a1 v) {  // n < 16
+  uint64_t lo = (uint64_t)v[0] | (uint64_t)v[1] << 32, hi = (uint64_t)v[2] | (uint64_t)v[3] << 32;
+  if (n & 8u) { *(u64_a1*)d = lo; d += 8; lo = hi; }
+  if (n & 4u) { *(u32_a1*)d = (uint32_t)lo; d += 4; lo >>= 32; }
+  if (n & 2u) { *(u16_a1*)d = (uint16_t)lo; d += 2; lo >>= 16; }
+  if (n & 1u) *d = (uint8_t)lo;
+}
+// 4 SEQ characters of the packed bytes b0 (high nibble first) and b1
+static __device__ __forceinline__ uint32_t seq4(uint32_t b0, uint32_t b1) {
+  // "=ACMGRSVTWYHKDBN" as two 8-byte halves for v_perm (selector byte = nibble & 7)
+  const uint32_t a0 = 0x4d43413du, a1 = 0x56535247u, a2 = 0x48595754u, a3 = 0x4e42444bu;
+  const uint32_t n0 = b0 >> 4, n1 = b0 & 15u, n2 = b1 >> 4, n3 = b1 & 15u;
+  const uint32_t sel = (n0 & 7u) | (n1 & 7u) << 8 | (n2 & 7u) << 16 | (n3 & 7u) << 24;
+  const uint32_t lo = __builtin_amdgcn_perm(a1, a0, sel), hi = __builtin_amdgcn_perm(a3, a2, sel);
+  const uint32_t m = ((n0 >> 3) * 0xffu) | ((n1 >> 3) * 0xffu) << 8 | ((n2 >> 3) * 0xffu) << 16 |
+                     ((n3 >> 3) * 0xffu) << 24;
+  return (lo & ~m) | (hi & m);
+}
+// 16 SEQ characters (or the first n < 16 of them) of the packed bytes at s (8 bytes read)
+static __device__ __forceinline__ u32x4_a1 seq16(const uint8_t* __restrict__ s) {
+  const uint64_t q = *(const u64_a1*)s;
+  u32x4_a1 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = seq4((uint32_t)(q >> (16 * j)) & 0xffu, (uint32_t)(q >> (16 * j + 8)) & 0xffu);
+  return o;
+}
 __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict__ u, uint64_t nrec,
                                                       const uint64_t* __restrict__ rec_off,
                                                       DevColumns c) {
-  const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63;
-  if (i >= nrec) return;
-  if (!c.layout_ok[i]) return;
-  const uint8_t* p = u + rec_off[i] + 36;
-  const uint32_t nl = c.name_len[i], nc = c.cigar_n[i], ls = c.seq_len[i], na = c.aux_len[i];
-  uint8_t* dn = c.names + c.name_off[i];
-  for (uint32_t k = lane; k < nl; k += 64) dn[k] = p[k];
-  p += nl;
-  uint32_t* dc = c.cigars + c.cigar_off[i];
-  for (uint32_t k = lane; k < nc; k += 64) dc[k] = ld_u32_unaligned(p + 4 * k);
-  p += 4 * nc;
-  uint8_t* ds = c.seq + c.seq_off[i];
-  const char* alpha = "=ACMGRSVTWYHKDBN";
-  for (uint32_t k = lane; k < ls; k += 64) {
-    const uint8_t b = p[k >> 1];
-    ds[k] = (uint8_t)alpha[(k & 1) ? (b & 15) : (b >> 4)];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t ntiles = (nrec + 63) / 64;
+  const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); t < ntiles; t += wstride) {
+    const uint64_t r = t * 64 + lane;
+    uint32_t nl = 0, nc = 0, ls = 0, na = 0;
+    uint64_t src = 0, o_name = 0, o_cig = 0, o_seq = 0, o_aux = 0;
+    if (r < nrec && c.layout_ok[r]) {
+      src = rec_off[r] + 36;
+      nl = c.name_len[r];
+      nc = c.cigar_n[r];
+      ls = c.seq_len[r];
+      na = c.aux_len[r];
+      o_name = c.name_off[r];
+      o_cig = c.cigar_off[r];
+      o_seq = c.seq_off[r];
+      o_aux = c.aux_off[r];
+    }
+    // field f: 0 names, 1 CIGAR bytes, 2 SEQ characters, 3 QUAL, 4 AUX
+#pragma unroll 1
+    for (uint32_t f = 0; f < 5; ++f) {
+      uint32_t len;
+      uint64_t s0, d0;
+      uint8_t* base;
+      if (f == 0) { len = nl; s0 = src; d0 = o_name; base = c.names; }
+      else if (f == 1) { len = 4u * nc; s0 = src + nl; d0 = 4 * o_cig; base = (uint8_t*)c.cigars; }
+      else if (f == 2) { len = ls; s0 = src + nl + 4u * nc; d0 = o_seq; base = c.seq; }
+      else if (f == 3) { len = ls; s0 = src + nl + 4u * nc + (ls + 1u) / 2u; d0 = o_seq; base = c.qual; }
+      else { len = na; s0 = src + nl + 4u * nc + (ls + 1u) / 2u + ls; d0 = o_aux; base = c.aux; }
+      const uint32_t units = (len + 15u) >> 4;
+      const uint32_t incl = wave_incl_sum(units, lane);
+      const uint32_t excl = incl - units;
+      const uint32_t total = __shfl(incl, 63);
+      // all 64 lanes stay active through the shuffles (a lane past the last unit reads but
+      // does not write), so no shuffle reads a lane the exec mask has switched off
+      for (uint32_t q0 = 0; q0 < total; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        // the record of unit q: the last lane whose first unit is <= q
+        uint32_t lo = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+          const uint32_t m = lo + step;
+          if (__shfl(excl, m) <= q) lo = m;
+        }
+        const uint32_t k = q - __shfl(excl, lo);      // unit index inside the segment
+        const uint32_t n = __shfl(len, lo) - 16u * k;  // bytes left in the segment
+        const uint64_t sq = __shfl(s0, lo), dq = __shfl(d0, lo);
+        if (q < total) {
+          uint8_t* dp = base + dq + 16u * k;
+          // 16 SEQ characters come from 8 packed bytes; over-reads stay in ubuf + slack
+          const u32x4_a1 v = f == 2 ? seq16(u + sq + 8u * k) : *(const u32x4_a1*)(u + sq + 16u * k);
+          if (n >= 16u) *(u32x4_a1*)dp = v;
+          else st_part(dp, n, v);
+        }
+      }
+    }
   }
-  p += (ls + 1) / 2;
-  uint8_t* dq = c.qual + c.seq_off[i];
-  for (uint32_t k = lane; k < ls; k += 64) dq[k] = p[k];
-  p += ls;
-  uint8_t* da = c.aux + c.aux_off[i];
-  for (uint32_t k = lane; k < na; k += 64) da[k] = p[k];
 }
 
 // ------------------------------------------------------------------------------------

@@ -144,26 +144,27 @@ __global__ __launch_bounds__(RS_WG) void k_gather_records(const uint8_t* __restr
                                                           uint64_t n,
                                                           const uint64_t* __restrict__ out_off,
                                                           uint8_t* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * (RS_WG / 64) + (threadIdx.x >> 6);
-  if (i >= n) return;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t src = rec_off[perm ? perm[i] : i];
-  const uint64_t dst = out_off[i];
-  const uint32_t len = (uint32_t)(out_off[i + 1] - dst);
-  const uint8_t* s = ubuf + src;
-  uint8_t* d = out + dst;
-  if (((src ^ dst) & 3u) == 0) {
-    // co-aligned: bytes up to the first dword boundary, dwords, then the tail
-    const uint32_t head = (uint32_t)((4u - (dst & 3u)) & 3u) < len ? (uint32_t)((4u - (dst & 3u)) & 3u) : len;
-    if (lane < head) d[lane] = s[lane];
-    const uint32_t nw = (len - head) >> 2;
-    const uint32_t* s4 = (const uint32_t*)(s + head);
-    uint32_t* d4 = (uint32_t*)(d + head);
-    for (uint32_t k = lane; k < nw; k += 64) d4[k] = s4[k];
-    const uint32_t t0 = head + 4u * nw;
-    if (t0 + lane < len) d[t0 + lane] = s[t0 + lane];
-  } else {
-    for (uint32_t k = lane; k < len; k += 64) d[k] = s[k];
+  for (uint64_t i = (uint64_t)blockIdx.x * (RS_WG / 64) + (threadIdx.x >> 6); i < n;
+       i += (uint64_t)gridDim.x * (RS_WG / 64)) {
+    const uint64_t src = rec_off[perm ? perm[i] : i];
+    const uint64_t dst = out_off[i];
+    const uint32_t len = (uint32_t)(out_off[i + 1] - dst);
+    const uint8_t* s = ubuf + src;
+    uint8_t* d = out + dst;
+    if (((src ^ dst) & 3u) == 0) {
+      // co-aligned: bytes up to the first dword boundary, dwords, then the tail
+      const uint32_t head = (uint32_t)((4u - (dst & 3u)) & 3u) < len ? (uint32_t)((4u - (dst & 3u)) & 3u) : len;
+      if (lane < head) d[lane] = s[lane];
+      const uint32_t nw = (len - head) >> 2;
+      const uint32_t* s4 = (const uint32_t*)(s + head);
+      uint32_t* d4 = (uint32_t*)(d + head);
+      for (uint32_t k = lane; k < nw; k += 64) d4[k] = s4[k];
+      const uint32_t t0 = head + 4u * nw;
+      if (t0 + lane < len) d[t0 + lane] = s[t0 + lane];
+    } else {
+      for (uint32_t k = lane; k < len; k += 64) d[k] = s[k];
+    }
   }
 }
 

@@ -261,6 +261,55 @@ def record_payloads(cols):
     return out, off
 
 
+_SEQ_ALPHA = np.frombuffer(b"=ACMGRSVTWYHKDBN", dtype=np.uint8)
+
+
+def _gather(src, starts, lens):
+    """concatenation of src[starts[i]:starts[i]+lens[i]] over i (vectorised)"""
+    lens = np.asarray(lens, np.int64)
+    tot = int(lens.sum())
+    if tot == 0:
+        return np.zeros(0, src.dtype), np.zeros(0, np.int64)
+    excl = np.cumsum(lens) - lens
+    k = np.arange(tot, dtype=np.int64) - np.repeat(excl, lens)  # index inside the segment
+    return src[np.repeat(np.asarray(starts, np.int64), lens) + k], k
+
+
+def pools(cols):
+    """The lazy getters' decoded fields of every record of a read_split result, concatenated in
+    record order (BAMRecord.getReadName / getCigar / getReadBases / getBaseQualities /
+    attributes): read names incl. NUL, CIGAR u32s, SEQ as
+    "=ACMGRSVTWYHKDBN" characters (high nibble first), QUAL, AUX bytes; plus layout_ok (the
+    variable block holds name + CIGAR + SEQ + QUAL).  Vectorised numpy (tests/helpers.py
+    has a per-record loop form of the same)."""
+    var = cols["var"]
+    vo = cols["var_off"].astype(np.int64)
+    L = cols["l_read_name"].astype(np.int64)
+    nc = cols["n_cigar"].astype(np.int64)
+    ls = cols["l_seq"].astype(np.int64)
+    vlen = vo[1:] - vo[:-1]
+    fixed = L + 4 * nc + (ls + 1) // 2 + ls
+    ok = (ls >= 0) & (fixed <= vlen)
+    L, nc, ls = np.where(ok, L, 0), np.where(ok, nc, 0), np.where(ok, ls, 0)
+    na = np.where(ok, vlen - fixed, 0)
+    s_name = vo[:-1]
+    s_cig = s_name + L
+    s_seq = s_cig + 4 * nc
+    s_qual = s_seq + (ls + 1) // 2
+    s_aux = s_qual + ls
+    names, _ = _gather(var, s_name, L)
+    cig, _ = _gather(var, s_cig, 4 * nc)
+    packed, k = _gather(var, s_seq, ls)  # one entry per character: k = character index
+    byte = var[np.repeat(s_seq, ls) + k // 2] if len(k) else np.zeros(0, np.uint8)
+    nib = np.where(k % 2 == 0, byte >> 4, byte & 15)
+    qual, _ = _gather(var, s_qual, ls)
+    aux, _ = _gather(var, s_aux, na)
+    return dict(layout_ok=ok.astype(np.uint8), names=names.astype(np.uint8),
+                cigars=np.ascontiguousarray(cig.astype(np.uint8)).view(np.uint32),
+                seq=_SEQ_ALPHA[nib] if len(nib) else np.zeros(0, np.uint8),
+                qual=qual.astype(np.uint8), aux=aux.astype(np.uint8))
+
+
 def sort_order(keys):
     """Sort's total order over LongWritable keys (signed i64 comparator, Sort.java:149-157 +
     TotalOrderPartitioner; identity reduce).  The reference leaves ties unspecified; the

@@ -218,3 +218,16 @@ def test_file_splits_slop(oracle_mod):
     assert len(b) == 11 and e[-1] == 1050 and b[-1] == 1000
     b, e = oracle_mod.file_splits(1010, 100)
     assert len(b) == 10 and b[-1] == 900 and e[-1] == 1010
+
+
+@pytest.mark.parametrize("name", sorted(_golden().keys()))
+def test_vectorised_pools_match_per_record_restatement(oracle_mod, name):
+    """oracle.pools (numpy, used by bench.py's parity at size) equals the per-record loop of
+    tests/helpers.py on every golden file, incl. records whose layout does not fit."""
+    from helpers import oracle_pools
+    data = np.fromfile(os.path.join(GOLDEN, name), dtype=np.uint8)
+    h = oracle_mod.read_header(data)
+    r = oracle_mod.read_split(data, h["first_voffset"], (len(data) << 16) | 0xffff)
+    a, b = oracle_mod.pools(r), oracle_pools(r)
+    for k in ("layout_ok", "names", "cigars", "seq", "qual", "aux"):
+        assert a[k].dtype == b[k].dtype and np.array_equal(a[k], b[k]), k
