@@ -1005,6 +1005,8 @@ __global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,
 // segment shorter, written in 8/4/2/1-byte pieces, so a neighbour's bytes in the pool are never
 // written); the tile's units are numbered by a wave scan and the lanes take consecutive units,
 // so a wave instruction moves ~1 KiB of consecutive pool bytes from a nearly consecutive source.
+// Unit size A/B at 5 GB: 8 B 10.1 ms, 16 B 8.3 ms, 32 B 14.2 ms
+// (profiles/r03/ab/pools_unit_5g.txt, pools_unit8_5g.txt).
 // (r02: one wave per record with byte copies, latency-bound, and a grid of 64 x records threads
 // that passed 2^32 above 67 M records; one thread per record with 16-byte copies: 59.7 ms per
 // 10 GB shard, every store instruction touching 64 lines.)
@@ -1028,6 +1030,9 @@ static __device__ __forceinline__ uint32_t seq4(uint32_t b0, uint32_t b1) {
                      ((n3 >> 3) * 0xffu) << 24;
   return (lo & ~m) | (hi & m);
 }
+#ifndef HBAM_AB_TAILFULL
+#define HBAM_AB_TAILFULL 0
+#endif
 // 16 SEQ characters (or the first n < 16 of them) of the packed bytes at s (8 bytes read)
 static __device__ __forceinline__ u32x4_a1 seq16(const uint8_t* __restrict__ s) {
   const uint64_t q = *(const u64_a1*)s;
@@ -1090,8 +1095,15 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
           uint8_t* dp = base + dq + 16u * k;
           // 16 SEQ characters come from 8 packed bytes; over-reads stay in ubuf + slack
           const u32x4_a1 v = f == 2 ? seq16(u + sq + 8u * k) : *(const u32x4_a1*)(u + sq + 16u * k);
-          if (n >= 16u) *(u32x4_a1*)dp = v;
-          else st_part(dp, n, v);
+          if (n >= 16u) {
+            *(u32x4_a1*)dp = v;
+          } else {
+#if HBAM_AB_TAILFULL
+            *(u32x4_a1*)dp = v;  // A/B build only (wrong bytes past the segment): tail cost
+#else
+            st_part(dp, n, v);
+#endif
+          }
         }
       }
     }
