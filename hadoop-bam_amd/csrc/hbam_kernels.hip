@@ -1030,9 +1030,6 @@ static __device__ __forceinline__ uint32_t seq4(uint32_t b0, uint32_t b1) {
                      ((n3 >> 3) * 0xffu) << 24;
   return (lo & ~m) | (hi & m);
 }
-#ifndef HBAM_AB_TAILFULL
-#define HBAM_AB_TAILFULL 0
-#endif
 // 16 SEQ characters (or the first n < 16 of them) of the packed bytes at s (8 bytes read)
 static __device__ __forceinline__ u32x4_a1 seq16(const uint8_t* __restrict__ s) {
   const uint64_t q = *(const u64_a1*)s;
@@ -1095,15 +1092,10 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
           uint8_t* dp = base + dq + 16u * k;
           // 16 SEQ characters come from 8 packed bytes; over-reads stay in ubuf + slack
           const u32x4_a1 v = f == 2 ? seq16(u + sq + 8u * k) : *(const u32x4_a1*)(u + sq + 16u * k);
-          if (n >= 16u) {
-            *(u32x4_a1*)dp = v;
-          } else {
-#if HBAM_AB_TAILFULL
-            *(u32x4_a1*)dp = v;  // A/B build only (wrong bytes past the segment): tail cost
-#else
-            st_part(dp, n, v);
-#endif
-          }
+          // (the pieces of the last unit cost 0.5 of 8.3 ms at 5 GB against full 16-byte stores:
+          // profiles/r03/ab/pools_tail_cost_5g.txt)
+          if (n >= 16u) *(u32x4_a1*)dp = v;
+          else st_part(dp, n, v);
         }
       }
     }
