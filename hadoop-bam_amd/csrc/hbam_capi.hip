@@ -210,10 +210,10 @@ int ensure(hbam_ctx* c, BufId id, size_t count, T** out) {
   size_t bytes = count * sizeof(T) + 64;
   Buf& b = c->bufs[id];
   if (b.cap < bytes) {
+    size_t want = std::max(bytes, b.cap + b.cap / 2);  // grow geometrically
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.cap = 0;
-    size_t want = std::max(bytes, b.cap + b.cap / 2);
     hipError_t e = hipMalloc(&b.p, want);
     if (e != hipSuccess) {
       (void)hipGetLastError();

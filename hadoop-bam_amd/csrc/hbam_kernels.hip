@@ -39,7 +39,9 @@ static __device__ __forceinline__ uint16_t ld_u16_unaligned(const uint8_t* p) { 
 // length is BSIZE (u16 @16) + 1.  One workgroup scans a SCAN_CHUNK-byte chunk; candidates
 // are collected in LDS, sorted, and written to a per-chunk slot (cap SCAN_CAP).
 // ------------------------------------------------------------------------------------
-// Candidate test of the 16 positions [p0, p0 + 16): bit k set when p0 + k can start a block.
+// Candidate test of the 16 positions [p0, p0 + 16): bit k set when p0 + k can start a block
+// (the two-pass fallback; k_scan_chunks keeps its inline form: written with this helper it ran
+// 1.59 -> 1.85 ms at 5 GB, profiles/r03/ab/pools_ilp_and_scan_5g.txt).
 __device__ __forceinline__ uint32_t scan_mask16(const uint8_t* __restrict__ comp, uint64_t p0, uint64_t end) {
   // (two 16-byte loads instead of the dword loads: 3.07 -> 3.34 ms per 10 GB, not kept)
   uint32_t w[7];
@@ -71,16 +73,29 @@ __global__ __launch_bounds__(256) void k_scan_chunks(const uint8_t* __restrict__
   const uint64_t c0 = begin + chunk * SCAN_CHUNK;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
-  // each thread tests 16 consecutive positions per step using a 36-byte window
+  // each thread tests 16 consecutive positions per step using a 32-byte window
   for (uint32_t step = 0; step < SCAN_CHUNK / (256 * 16); ++step) {
     const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * 16;
     if (p0 >= end) break;
-    uint32_t mask = scan_mask16(comp, p0, end);
-    while (mask) {
-      const uint32_t k = __ffs(mask) - 1u;
-      mask &= mask - 1u;
-      const uint32_t i = atomicAdd(&s_cnt, 1u);
-      if (i < SCAN_CAP) s_pos[i] = p0 + k;
+    // 16-byte aligned relative to comp (begin is 16-aligned by construction of callers? no:
+    // use byte loads for the window to stay alignment-agnostic)
+    uint32_t w[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint64_t p = p0 + k;
+      if (p + 18 > end) break;
+      // bytes p..p+3 and p+10..p+11
+      const int q = k >> 2, r = k & 3;
+      const uint64_t lo = (uint64_t)w[q] | (uint64_t)w[q + 1] << 32;
+      const uint32_t m = (uint32_t)(lo >> (8 * r));
+      const uint64_t lo2 = (uint64_t)w[(k + 8) >> 2] | (uint64_t)w[((k + 8) >> 2) + 1] << 32;
+      const uint32_t x = (uint32_t)(lo2 >> (8 * ((k + 8) & 3)));  // bytes p+8..p+11
+      if (m == 0x04088b1fu && (x >> 16) == 6u) {
+        const uint32_t i = atomicAdd(&s_cnt, 1u);
+        if (i < SCAN_CAP) s_pos[i] = p;
+      }
     }
   }
   __syncthreads();
@@ -1075,7 +1090,9 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
       const uint32_t excl = incl - units;
       const uint32_t total = __shfl(incl, 63);
       // all 64 lanes stay active through the shuffles (a lane past the last unit reads but
-      // does not write), so no shuffle reads a lane the exec mask has switched off
+      // does not write): ds_bpermute does not return the value of a lane the exec mask has
+      // switched off (a build with one shuffle under `q < total` corrupted names and AUX).
+      // Two or four units per lane per step, loads first: 8.7 / 9.9 vs 8.3 ms at 5 GB.
       for (uint32_t q0 = 0; q0 < total; q0 += 64) {
         const uint32_t q = q0 + lane;
         // the record of unit q: the last lane whose first unit is <= q
