@@ -1045,9 +1045,6 @@ static __device__ __forceinline__ uint32_t seq4(uint32_t b0, uint32_t b1) {
                      ((n3 >> 3) * 0xffu) << 24;
   return (lo & ~m) | (hi & m);
 }
-#ifndef HBAM_POOL_UNIFORM
-#define HBAM_POOL_UNIFORM 1  // A/B: division instead of the search for uniform tiles
-#endif
 // 16 SEQ characters (or the first n < 16 of them) of the packed bytes at s (8 bytes read)
 static __device__ __forceinline__ u32x4_a1 seq16(const uint8_t* __restrict__ s) {
   const uint64_t q = *(const u64_a1*)s;
@@ -1096,25 +1093,16 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
       // does not write): ds_bpermute does not return the value of a lane the exec mask has
       // switched off (a build with one shuffle under `q < total` corrupted names and AUX).
       // Two or four units per lane per step, loads first: 8.7 / 9.9 vs 8.3 ms at 5 GB.
-      // When every record of the tile has the same unit count (fixed-length reads: SEQ and QUAL
-      // nearly always), unit q belongs to record q / u0 (exact as q * ceil(2^32 / u0) >> 32 for
-      // q < 64 * u0, u0 < 8192); otherwise a 6-step shuffle search.  The test is wave-uniform.
-      const uint32_t u0 = __shfl(units, 0);
-      const bool same = HBAM_POOL_UNIFORM && u0 != 0u && u0 < 8192u && __all(units == u0);
-      const uint64_t magic = same ? ((1ull << 32) + u0 - 1u) / u0 : 0ull;
+      // (a division instead of the search for tiles whose records all have the same unit count:
+      // 8.42 vs 8.20 ms at 5 GB, profiles/r03/ab/pools_uniform_tile_division_5g.txt; not kept)
       for (uint32_t q0 = 0; q0 < total; q0 += 64) {
         const uint32_t q = q0 + lane;
         // the record of unit q: the last lane whose first unit is <= q
         uint32_t lo = 0;
-        if (same) {
-          lo = (uint32_t)(((uint64_t)q * magic) >> 32);
-          lo = lo < 63u ? lo : 63u;
-        } else {
 #pragma unroll
-          for (uint32_t step = 32; step; step >>= 1) {
-            const uint32_t m = lo + step;
-            if (__shfl(excl, m) <= q) lo = m;
-          }
+        for (uint32_t step = 32; step; step >>= 1) {
+          const uint32_t m = lo + step;
+          if (__shfl(excl, m) <= q) lo = m;
         }
         const uint32_t k = q - __shfl(excl, lo);      // unit index inside the segment
         const uint32_t n = __shfl(len, lo) - 16u * k;  // bytes left in the segment
