@@ -917,6 +917,14 @@ __global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nrec) return;
   const uint64_t r = rec_off[i];
+  // every fixed field read up front (ubuf + slack holds r + 36 for any record start), so one
+  // memory round trip follows rec_off instead of two (block_size, then the fields)
+  const uint8_t* p = u + r;
+  const int32_t bs0 = (int32_t)ld_u32_unaligned(p), ref0 = (int32_t)ld_u32_unaligned(p + 4),
+                pos0 = (int32_t)ld_u32_unaligned(p + 8);
+  const uint32_t w12 = ld_u32_unaligned(p + 12), w16 = ld_u32_unaligned(p + 16);
+  const int32_t lseq0 = (int32_t)ld_u32_unaligned(p + 20), nref0 = (int32_t)ld_u32_unaligned(p + 24),
+                npos0 = (int32_t)ld_u32_unaligned(p + 28), tlen0 = (int32_t)ld_u32_unaligned(p + 32);
   int32_t st = ST_OK;
   // split bound (nextKeyValue :173): checked before decode()
   if ((int64_t)voffset[i] >= (int64_t)v_end) {
@@ -928,7 +936,7 @@ __global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,
   }
   int32_t bs = 0;
   if (st == ST_OK) {
-    bs = (int32_t)ld_u32_unaligned(u + r);
+    bs = bs0;
     if (bs < 32) st = HBAM_EFORMAT;
   }
   if (st == ST_OK && nev) {
@@ -948,18 +956,17 @@ __global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,
   uint8_t lrn = 0, mapq = 0;
   uint16_t bin = 0, ncig = 0, flag = 0;
   if (st == ST_OK) {
-    const uint8_t* p = u + r;
-    ref = (int32_t)ld_u32_unaligned(p + 4);
-    pos = (int32_t)ld_u32_unaligned(p + 8);
-    lrn = p[12];
-    mapq = p[13];
-    bin = ld_u16_unaligned(p + 14);
-    ncig = ld_u16_unaligned(p + 16);
-    flag = ld_u16_unaligned(p + 18);
-    lseq = (int32_t)ld_u32_unaligned(p + 20);
-    nref = (int32_t)ld_u32_unaligned(p + 24);
-    npos = (int32_t)ld_u32_unaligned(p + 28);
-    tlen = (int32_t)ld_u32_unaligned(p + 32);
+    ref = ref0;
+    pos = pos0;
+    lrn = (uint8_t)w12;
+    mapq = (uint8_t)(w12 >> 8);
+    bin = (uint16_t)(w12 >> 16);
+    ncig = (uint16_t)w16;
+    flag = (uint16_t)(w16 >> 16);
+    lseq = lseq0;
+    nref = nref0;
+    npos = npos0;
+    tlen = tlen0;
     if (validate_refs && ((ref != -1 && (ref < 0 || ref >= n_ref)) ||
                           (nref != -1 && (nref < 0 || nref >= n_ref))))
       st = HBAM_EREFID;
@@ -1092,9 +1099,12 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
       // all 64 lanes stay active through the shuffles (a lane past the last unit reads but
       // does not write): ds_bpermute does not return the value of a lane the exec mask has
       // switched off (a build with one shuffle under `q < total` corrupted names and AUX).
-      // Two or four units per lane per step, loads first: 8.7 / 9.9 vs 8.3 ms at 5 GB.
-      // (a division instead of the search for tiles whose records all have the same unit count:
-      // 8.42 vs 8.20 ms at 5 GB, profiles/r03/ab/pools_uniform_tile_division_5g.txt; not kept)
+      // Not kept (profiles/r03/ab/pools_*_5g.txt, 5 GB): two or four units per lane per step,
+      // loads first, 8.7 / 9.9 vs 8.3 ms; a division in place of the search for tiles whose
+      // records all have the same unit count, 8.4 vs 8.2; software-pipelined by one unit, 8.6
+      // vs 8.5; all five fields' units numbered together in source order (every line of the
+      // record stream fetched once: FETCH 75.5 -> 29.9 GB per 10 GB shard, WRITE 30.6 -> 36.2),
+      // 8.8 vs 8.5 ms.  The kernel is bound by its per-unit latency, not by HBM traffic.
       for (uint32_t q0 = 0; q0 < total; q0 += 64) {
         const uint32_t q = q0 + lane;
         // the record of unit q: the last lane whose first unit is <= q

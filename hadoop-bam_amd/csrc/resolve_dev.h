@@ -163,6 +163,8 @@ __device__ __forceinline__ void rs_copy_glb(uint8_t* __restrict__ buf, uint32_t 
     // byte-aligned 8-byte global loads (the device runs in unaligned access mode)
     // (requesting only the words a match covers, as exec-masked loads, ran slower: 21.45 ->
     // 22.2 ms at 5 GB, profiles/r03/ab/resolve_condld_5g.txt)
+    // (as two 16-byte loads: 21.34 vs 21.39 ms at 5 GB, no gain;
+    // profiles/r03/ab/decode_fixed_hoist_and_resolve_g16_5g.txt)
     const uint64_t v0 = *(const uint64_t*)(g + t), v1 = *(const uint64_t*)(g + t + 8),
                    v2 = *(const uint64_t*)(g + t + 16), v3 = *(const uint64_t*)(g + t + 24);
     const uint32_t n = len - t;
