@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 3, call T: closing check of the tree — GPU suite, config #2 bench line, rocprof kernel
+# Round 3, call T (re-run on the final tree): closing check — GPU suite, config #2 bench line, rocprof kernel
 # stats of the same command, smoke.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r3t
+O=gpurun_out/r3t2
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/tests.txt 2>&1; echo "rc $?" >> $O/tests.txt
