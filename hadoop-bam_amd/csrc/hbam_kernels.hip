@@ -476,62 +476,8 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
     // (A/B at 10 GB without this drain: 58.8 vs 58.6 ms, so it stays)
     if (s0 >= RS_W) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t lds_from = s0 - RS_W - a0;  // block offset of LDS index 0 (when s0 >= RS_W)
-#if HBAM_RS_UNITS
-    // 16-byte units of the pre matches numbered over the lanes (a wave scan per 64 matches,
-    // a unit's match found by a 6-step shuffle search), so a lane copies one unit per step
-    // whatever the matches' lengths.  A match that overlaps itself (dist < len: only one that
-    // starts at s0 can be "pre") takes the per-match path.
-    for (uint32_t j0 = 0; j0 < npre; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      uint32_t p = 0, len = 0, dist = 1;
-      if (j < npre) {
-        const uint64_t rec = rs_unpack(s_rec[j], s_pos);
-        p = (uint32_t)rec & 0xffffu;
-        len = (uint32_t)(rec >> 16) & 0xffffu;
-        dist = (uint32_t)(rec >> 32) & 0xffffu;
-      }
-      const bool ovl = dist < len;
-      if (ovl) rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
-      const uint32_t units = ovl ? 0u : (len + 15u) >> 4;
-      const uint32_t incl = wave_incl_sum(units, lane);
-      const uint32_t excl = incl - units;
-      const uint32_t total = __shfl(incl, 63);
-      for (uint32_t q0 = 0; q0 < total; q0 += 64) {  // every lane active through the shuffles
-        const uint32_t q = q0 + lane;
-        uint32_t lo = 0;
-#pragma unroll
-        for (uint32_t step = 32; step; step >>= 1) {
-          const uint32_t m = lo + step;
-          if (__shfl(excl, m) <= q) lo = m;
-        }
-        const uint32_t k = q - __shfl(excl, lo);
-        const uint32_t P = __shfl(p, lo), L = __shfl(len, lo), D = __shfl(dist, lo);
-        if (q < total) {
-          const uint32_t x = P + 16u * k, sx = x - D;
-          const uint32_t n = L - 16u * k < 16u ? L - 16u * k : 16u;
-          rs_u4_a1 v;
-          if (s0 < RS_W || sx >= lds_from) {
-            v = *(const rs_u4_a1*)(s_buf + lbase + sx);  // window in LDS
-          } else {
-            v = *(const rs_u4_a1*)(ubuf + base + sx);  // written back: global
-            const uint32_t g = lds_from - sx;          // bytes before the LDS window
-            if (g < n) {                               // straddles the window start
-              const rs_u4_a1 b = *(const rs_u4_a1*)(s_buf + lbase + sx);
-#pragma unroll
-              for (uint32_t w = 0; w < 4; ++w) {
-                const uint32_t lo8 = 4u * w;
-                const uint32_t m = g >= lo8 + 4u ? ~0u : g <= lo8 ? 0u : (1u << (8u * (g - lo8))) - 1u;
-                v[w] = (v[w] & m) | (b[w] & ~m);
-              }
-            }
-          }
-          uint8_t* d = s_buf + lbase + x;
-          lds_wr_part(d, (uint64_t)v[0] | (uint64_t)v[1] << 32, n < 8u ? n : 8u);
-          if (n > 8u) lds_wr_part(d + 8, (uint64_t)v[2] | (uint64_t)v[3] << 32, n - 8u);
-        }
-      }
-    }
-#else
+    // (pre-match copies as 16-byte units numbered over the lanes, as the pools kernel does: a
+    // first build ran 23.4 vs 21.4 ms at 5 GB and was not pursued, profiles/r03/ab/resolve_units_5g.txt)
     for (uint32_t j = lane; j < npre; j += 64) {
       const uint64_t rec = rs_unpack(s_rec[j], s_pos);
       const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
@@ -545,7 +491,6 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
         if (gl < len) rs_copy_lds(s_buf, lbase + p + gl, len - gl, dist, s_sel);
       }
     }
-#endif
 #ifdef HBAM_PROF
     p_pre += PROF_CLK() - q1;
 #endif

@@ -32,10 +32,6 @@ namespace hbam {
 #ifndef HBAM_RS_S
 #define HBAM_RS_S 1024  // A/B at 2 GB (window 1 KiB): 2048 -> 16.8 ms, 1024 -> 11.7 ms
 #endif
-#ifndef HBAM_RS_UNITS
-#define HBAM_RS_UNITS 0  // A/B: pre-match copies as 16-byte units numbered over the lanes
-#endif
-typedef uint32_t rs_u4_a1 __attribute__((ext_vector_type(4), aligned(1)));  // 16 B, any address
 constexpr uint32_t RS_S = HBAM_RS_S;                  // stretch (output bytes): 1024 or 2048
 constexpr uint32_t RS_C = RS_S / 1024;                // 16-byte columns per lane per stretch
 constexpr uint32_t RS_W = HBAM_RS_W;                  // window kept in LDS behind the stretch
