@@ -22,6 +22,11 @@
  * (BGZF block with ISIZE > 65536), HBAM_EDEVICE (HIP error), HBAM_EINVAL, HBAM_EMORE
  * (the compressed window handed in ends before the split's last record).
  *
+ * Inputs: an argument with `on_device` = 0 is host memory, copied in by the call; with
+ * `on_device` = 1 it is a device pointer read in place, and the kernels read whole 16-byte
+ * quads and fixed-size windows past the last byte, so 64 readable bytes must follow `len`
+ * (their contents do not matter).  Host inputs get that padding from the library.
+ *
  * Threading: a context owns one HIP stream and is single-threaded; separate contexts
  * (one per Hadoop task thread) are independent.  Device buffers returned in
  * hbam_columns are owned by the context and stay valid until the next decode call on
