@@ -39,9 +39,6 @@ static __device__ __forceinline__ uint16_t ld_u16_unaligned(const uint8_t* p) { 
 // length is BSIZE (u16 @16) + 1.  One workgroup scans a SCAN_CHUNK-byte chunk; candidates
 // are collected in LDS, sorted, and written to a per-chunk slot (cap SCAN_CAP).
 // ------------------------------------------------------------------------------------
-#ifndef HBAM_SCAN_PF
-#define HBAM_SCAN_PF 0
-#endif
 // Candidate test of the 16 positions [p0, p0 + 16): bit k set when p0 + k can start a block
 // (the two-pass fallback; k_scan_chunks keeps its inline form: written with this helper it ran
 // 1.59 -> 1.85 ms at 5 GB, profiles/r03/ab/pools_ilp_and_scan_5g.txt).
@@ -77,35 +74,16 @@ __global__ __launch_bounds__(256) void k_scan_chunks(const uint8_t* __restrict__
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   // each thread tests 16 consecutive positions per step using a 32-byte window
-#if HBAM_SCAN_PF
-  // A/B: the next step's window is requested before this step's positions are tested
-  uint32_t wn[9];
-  {
-    const uint64_t q0 = c0 + (uint64_t)threadIdx.x * 16;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) wn[i] = q0 < end ? ld_u32_unaligned(comp + q0 + 4 * i) : 0u;
-  }
-#endif
+  // (requesting the next step's window before testing this one: 1.56 -> 1.71 ms at 5 GB,
+  // profiles/r03/ab/scan_prefetch_5g.txt; not kept)
   for (uint32_t step = 0; step < SCAN_CHUNK / (256 * 16); ++step) {
     const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * 16;
     if (p0 >= end) break;
     // 16-byte aligned relative to comp (begin is 16-aligned by construction of callers? no:
     // use byte loads for the window to stay alignment-agnostic)
     uint32_t w[9];
-#if HBAM_SCAN_PF
-#pragma unroll
-    for (int i = 0; i < 9; ++i) w[i] = wn[i];
-    {
-      const uint64_t q0 = p0 + 256 * 16;
-      if (step + 1 < SCAN_CHUNK / (256 * 16) && q0 < end) {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) wn[i] = ld_u32_unaligned(comp + q0 + 4 * i);
-      }
-    }
-#else
 #pragma unroll
     for (int i = 0; i < 9; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
-#endif
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const uint64_t p = p0 + k;
