@@ -3,7 +3,7 @@
 # stats of the same command, smoke.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r3t2
+O=gpurun_out/r3t3
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/tests.txt 2>&1; echo "rc $?" >> $O/tests.txt
