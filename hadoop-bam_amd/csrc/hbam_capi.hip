@@ -160,6 +160,13 @@ enum BufId {
   // BCF read path (hbam_bcf_api.hip)
   B_BCF_COLS,
   B_BCF_SCRATCH,
+  // Sort exchange over RCCL (hbam_comm.hip): receive buffers, counts, samples
+  B_X_KEY,
+  B_X_VOFF,
+  B_X_BS,
+  B_X_PAY,
+  B_X_CNT,
+  B_X_SAMP,
   B_COUNT_ALL
 };
 
@@ -1176,7 +1183,14 @@ struct hbam_split_stream {
   hbam_ctx* c = nullptr;
   const uint8_t* file = nullptr;
   uint64_t file_len = 0, v_cur = 0, v_end = 0, win = 0;
+  uint64_t limit = 0;  // no window reaches past this file offset (split-local reads, see split_limit)
   int32_t n_ref = 0;
+  // read-callback streams (hbam_split_open_reader): pinned host staging per window slot
+  hbam_read_fn read = nullptr;
+  void* user = nullptr;
+  uint8_t* hbuf[2] = {nullptr, nullptr};
+  uint64_t hcap[2] = {0, 0};
+  uint64_t read_bytes = 0;  // bytes requested from the callback
   uint8_t* dbuf[2] = {nullptr, nullptr};
   uint64_t dcap[2] = {0, 0};
   uint64_t base[2] = {0, 0}, len[2] = {0, 0};
@@ -1203,11 +1217,54 @@ int stream_wait(hbam_split_stream* s, int k) {
   return HBAM_OK;
 }
 
+// Split-local bound: a FileVirtualSplit [v_start, v_end) reads records starting before v_end,
+// i.e. in blocks at coff <= v_end >> 16; the last of them may run into the next blocks, and the
+// reader stops at the first record at or after v_end, which starts in a block that begins within
+// 64 KiB after that.  Windows never reach past (v_end >> 16) + SPLIT_TAIL; when a window so cut
+// holds no complete record (a record longer than the tail) the bound moves out (hbam_split_next).
+constexpr uint64_t SPLIT_TAIL = 3ull << 16;
+uint64_t split_limit(uint64_t v_end, uint64_t file_len) {
+  const uint64_t e = v_end >> 16;
+  return e >= file_len || file_len - e <= SPLIT_TAIL ? file_len : e + SPLIT_TAIL;
+}
+
+// read-callback streams: file bytes [b, b + n) into host staging slot k — the part the other
+// slot's staging already holds (the windows' overlap) is copied from there, the rest read once
+int stream_stage(hbam_split_stream* s, int k, uint64_t b, uint64_t n) {
+  hbam_ctx* c = s->c;
+  if (s->hcap[k] < n + 64) {
+    if (s->hbuf[k]) HIPCHK(c, hipHostFree(s->hbuf[k]));
+    s->hbuf[k] = nullptr;
+    s->hcap[k] = 0;
+    if (hipHostMalloc((void**)&s->hbuf[k], n + 64, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return set_err(c, HBAM_ENOMEM, "hbam_split_next: hipHostMalloc(%llu) failed", (unsigned long long)(n + 64));
+    }
+    s->hcap[k] = n + 64;
+  }
+  uint64_t have = 0;
+  const int o = 1 - k;
+  if (s->valid[o] && s->hbuf[o] && s->base[o] <= b && b < s->base[o] + s->len[o]) {
+    have = std::min(n, s->base[o] + s->len[o] - b);
+    memcpy(s->hbuf[k], s->hbuf[o] + (b - s->base[o]), have);
+  }
+  while (have < n) {
+    const int64_t got = s->read(s->user, b + have, n - have, s->hbuf[k] + have);
+    if (got <= 0)
+      return set_err(c, HBAM_EIO, "hbam_split_next: read(%llu, %llu) returned %lld", (unsigned long long)(b + have),
+                     (unsigned long long)(n - have), (long long)got);
+    s->read_bytes += (uint64_t)got;
+    have += std::min<uint64_t>((uint64_t)got, n - have);
+  }
+  return HBAM_OK;
+}
+
 // copy file bytes [b, b + n) into window buffer k on the copy stream (asynchronous)
 int stream_copy(hbam_split_stream* s, int k, uint64_t b, uint64_t n) {
   hbam_ctx* c = s->c;
   int rc = stream_wait(s, k);
   if (rc) return rc;
+  if (s->read && n && (rc = stream_stage(s, k, b, n))) return rc;
   if (s->dcap[k] < n + 64) {
     if (s->dbuf[k]) HIPCHK(c, hipFree(s->dbuf[k]));
     s->dbuf[k] = nullptr;
@@ -1219,7 +1276,7 @@ int stream_copy(hbam_split_stream* s, int k, uint64_t b, uint64_t n) {
     s->dcap[k] = n + 64;
   }
   HIPCHK(c, hipEventRecord(s->e0[k], s->cs));
-  if (n) HIPCHK(c, hipMemcpyAsync(s->dbuf[k], s->file + b, n, hipMemcpyHostToDevice, s->cs));
+  if (n) HIPCHK(c, hipMemcpyAsync(s->dbuf[k], s->read ? s->hbuf[k] : s->file + b, n, hipMemcpyHostToDevice, s->cs));
   HIPCHK(c, hipMemsetAsync(s->dbuf[k] + n, 0, 64, s->cs));
   HIPCHK(c, hipEventRecord(s->e1[k], s->cs));
   s->base[k] = b;
@@ -1230,17 +1287,21 @@ int stream_copy(hbam_split_stream* s, int k, uint64_t b, uint64_t n) {
 }
 }  // namespace
 
-extern "C" hbam_split_stream* hbam_split_open(hbam_ctx* c, const uint8_t* file, uint64_t file_len,
-                                         uint64_t v_start, uint64_t v_end, int32_t n_ref,
-                                         uint64_t window_bytes) {
-  if (!c || (!file && file_len) || n_ref < 0) return nullptr;
+namespace {
+hbam_split_stream* split_open(hbam_ctx* c, const uint8_t* file, hbam_read_fn read, void* user,
+                              uint64_t file_len, uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                              uint64_t window_bytes) {
+  if (!c || n_ref < 0) return nullptr;
   if (hipSetDevice(c->device) != hipSuccess) return nullptr;
   hbam_split_stream* s = new hbam_split_stream();
   s->c = c;
   s->file = file;
+  s->read = read;
+  s->user = user;
   s->file_len = file_len;
   s->v_cur = v_start;
   s->v_end = v_end;
+  s->limit = split_limit(v_end, file_len);
   s->n_ref = n_ref;
   s->win = std::max<uint64_t>(window_bytes, 1 << 16);
   bool ok = hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking) == hipSuccess;
@@ -1253,6 +1314,21 @@ extern "C" hbam_split_stream* hbam_split_open(hbam_ctx* c, const uint8_t* file, 
   }
   return s;
 }
+}  // namespace
+
+extern "C" hbam_split_stream* hbam_split_open(hbam_ctx* c, const uint8_t* file, uint64_t file_len,
+                                         uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                                         uint64_t window_bytes) {
+  if (!file && file_len) return nullptr;
+  return split_open(c, file, nullptr, nullptr, file_len, v_start, v_end, n_ref, window_bytes);
+}
+
+extern "C" hbam_split_stream* hbam_split_open_reader(hbam_ctx* c, hbam_read_fn read, void* user,
+                                                     uint64_t file_len, uint64_t v_start, uint64_t v_end,
+                                                     int32_t n_ref, uint64_t window_bytes) {
+  if (!read) return nullptr;
+  return split_open(c, nullptr, read, user, file_len, v_start, v_end, n_ref, window_bytes);
+}
 
 extern "C" int hbam_split_next(hbam_split_stream* s, hbam_columns* out) {
   if (!s || !out) return HBAM_EINVAL;
@@ -1262,15 +1338,16 @@ extern "C" int hbam_split_next(hbam_split_stream* s, hbam_columns* out) {
   HIPCHK(c, hipSetDevice(c->device));
   for (;;) {
     const uint64_t ws = std::min(s->v_cur >> 16, s->file_len);
-    const uint64_t ahead = std::min<uint64_t>(s->win / 2, s->file_len - ws);
+    const uint64_t lim = std::max(s->limit, ws);
+    const uint64_t ahead = std::min<uint64_t>(s->win / 2, lim - ws);
     int k = -1;
     for (int b = 0; b < 2; ++b)
       if (s->valid[b] && s->base[b] <= ws && s->base[b] + s->len[b] >= ws + ahead &&
-          (ws < s->base[b] + s->len[b] || s->base[b] + s->len[b] == s->file_len))
+          (ws < s->base[b] + s->len[b] || s->base[b] + s->len[b] == lim))
         k = b;
     if (k < 0) {  // not predicted (first window, long record, grown window): copy it now
       k = s->valid[0] && !s->valid[1] ? 1 : 0;
-      int rc = stream_copy(s, k, ws, std::min(s->win, s->file_len - ws));
+      int rc = stream_copy(s, k, ws, std::min(s->win, lim - ws));
       if (rc) return rc;
     }
     int rc = stream_wait(s, k);
@@ -1278,11 +1355,11 @@ extern "C" int hbam_split_next(hbam_split_stream* s, hbam_columns* out) {
     // prefetch the predicted next window into the other buffer while this one decodes
     const uint64_t wend = s->base[k] + s->len[k];
     const int o = 1 - k;
-    if (wend < s->file_len) {
+    if (wend < lim) {
       const uint64_t ov = std::min<uint64_t>(STREAM_OVERLAP, s->win / 2);
       const uint64_t ps = std::max(s->base[k], wend > ov ? wend - ov : 0);
       if (!(s->valid[o] && s->base[o] == ps))
-        if ((rc = stream_copy(s, o, ps, std::min(s->win, s->file_len - ps)))) return rc;
+        if ((rc = stream_copy(s, o, ps, std::min(s->win, lim - ps)))) return rc;
     }
     ++s->windows;
     const uint8_t* w = s->dbuf[k] ? s->dbuf[k] : (const uint8_t*)s->dbuf[o];
@@ -1301,14 +1378,16 @@ extern "C" int hbam_split_next(hbam_split_stream* s, hbam_columns* out) {
     out->status = HBAM_OK;
     out->err_record = 0;
     if (resume == s->v_cur && out->n_records == 0) {
-      // not one record fits: a longer window, copied at the resume point
+      // not one record fits: a longer window, copied at the resume point (past the split-local
+      // bound too when the window was cut there)
       if (wend >= s->file_len)
         return set_err(c, HBAM_EINVAL, "hbam_split_next: no progress at voffset %llu", (unsigned long long)s->v_cur);
       for (int b = 0; b < 2; ++b) {
         if ((rc = stream_wait(s, b))) return rc;
         s->valid[b] = false;
       }
-      s->win *= 2;
+      if (wend >= lim) s->limit = std::min(s->file_len, lim + std::max<uint64_t>(s->win, SPLIT_TAIL));
+      else s->win *= 2;
       continue;
     }
     s->v_cur = resume;
@@ -1324,12 +1403,15 @@ extern "C" int hbam_split_stats(const hbam_split_stream* s, uint64_t* h2d_bytes,
   return HBAM_OK;
 }
 
+extern "C" uint64_t hbam_split_read_bytes(const hbam_split_stream* s) { return s ? s->read_bytes : 0; }
+
 extern "C" void hbam_split_close(hbam_split_stream* s) {
   if (!s) return;
   (void)hipSetDevice(s->c->device);
   if (s->cs) (void)hipStreamSynchronize(s->cs);
   for (int k = 0; k < 2; ++k) {
     if (s->dbuf[k]) (void)hipFree(s->dbuf[k]);
+    if (s->hbuf[k]) (void)hipHostFree(s->hbuf[k]);
     if (s->e0[k]) (void)hipEventDestroy(s->e0[k]);
     if (s->e1[k]) (void)hipEventDestroy(s->e1[k]);
   }
@@ -2247,3 +2329,4 @@ extern "C" int64_t hbam_bgzf_compress(hbam_ctx* c, const uint8_t* src, int src_o
 
 #include "hbam_consumers.hip"
 #include "hbam_bcf_api.hip"
+#include "hbam_comm.hip"

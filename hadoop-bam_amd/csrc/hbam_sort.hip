@@ -188,6 +188,16 @@ __global__ __launch_bounds__(RS_WG) void k_sort_bounds(const int64_t* __restrict
   byte_b[j] = offsets[lo];
 }
 
+// InputSampler stand-in of the exchange (Sort.java:154-157): regular
+// samples of a rank's sorted keys, out[0] = k = min(n, s), out[1 + j] = keys[j * n / k]
+__global__ __launch_bounds__(RS_WG) void k_sample_keys(const int64_t* __restrict__ keys, uint64_t n,
+                                                       uint32_t s, int64_t* __restrict__ out) {
+  const uint64_t k = n < (uint64_t)s ? n : (uint64_t)s;
+  const uint32_t j = blockIdx.x * RS_WG + threadIdx.x;
+  if (j == 0) out[0] = (int64_t)k;
+  if (j < s) out[1 + j] = j < k ? keys[(uint64_t)j * n / k] : 0;
+}
+
 // SplittingBAMIndexer (SplittingBAMIndexer.java:146-248): the voffset before every
 // granularity-th record (records counted from 1) of a whole-file decode
 __global__ __launch_bounds__(RS_WG) void k_index_pick(const uint64_t* __restrict__ voffset, uint64_t n,

@@ -11,7 +11,7 @@ from .formats import (  # noqa: F401
     AnySAMInputFormat, BAMInputFormat, BGZFBlockIndex, BGZFBlockIndexer, BGZFSplitFileInputFormat, BAMRecordReader, BAMSplitGuesser, BGZFSplitGuesser,
     Configuration, FileSplit, FileVirtualSplit, SAMRecordWritable, SplittingBAMIndex,
     SplittingBAMIndexer, compute_file_splits)
-from .sort import HipSortOps, SortedRun, sort_sharded  # noqa: F401
+from .sort import HipSortOps, RcclComm, SortedRun, sort_sharded  # noqa: F401
 from .output import (  # noqa: F401
     BAMRecordWriter, KeyIgnoringBAMOutputFormat, KeyIgnoringBAMRecordWriter, SAMFileHeader,
     SAMOutputPreparer, merge_sam_into, read_sam_header)

@@ -55,8 +55,13 @@ EXPORTS = [
     "hbam_guess_window_len", "hbam_guess_windows", "hbam_guess_bgzf_window_len",
     "hbam_guess_bgzf_window", "hbam_probabilistic_splits_windows", "hbam_merge_remap",
     "hbam_host_register", "hbam_host_unregister", "hbam_bcf_parse_header", "hbam_guess_bcf_window_len",
-    "hbam_guess_bcf_windows", "hbam_bcf_decode_split",
+    "hbam_guess_bcf_windows", "hbam_bcf_decode_split", "hbam_comm_unique_id", "hbam_comm_init",
+    "hbam_comm_destroy", "hbam_comm_split_points", "hbam_sort_exchange", "hbam_split_open_reader",
+    "hbam_split_read_bytes",
 ]
+
+# hbam_read_fn: int64_t read(void* user, uint64_t offset, uint64_t len, uint8_t* dst)
+READ_FN = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p)
 
 
 class HbamUnavailable(RuntimeError):
@@ -83,7 +88,7 @@ class Timing(C.Structure):
                                           "decode_ms", "pools_ms", "total_ms",
                                           "huffman_ms", "resolve_ms")] + \
                [(n, C.c_uint64) for n in ("n_blocks", "comp_bytes", "ubuf_bytes", "n_records",
-                                          "pool_bytes", "reserved")]
+                                          "pool_bytes")] + [("exchange_ms", C.c_double)]
 
 
 class SortedRunC(C.Structure):
@@ -210,6 +215,9 @@ def load(path=None):
         "hbam_resolve_tokens": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, C.c_uint32, _i32p]),
         "hbam_split_open": (vp, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64]),
         "hbam_split_next": (C.c_int, [vp, C.POINTER(Columns)]),
+        "hbam_split_open_reader": (vp, [vp, READ_FN, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int32,
+                                        C.c_uint64]),
+        "hbam_split_read_bytes": (C.c_uint64, [vp]),
         "hbam_split_stats": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_double),
                                        C.POINTER(C.c_uint64)]),
         "hbam_split_close": (None, [vp]),
@@ -233,6 +241,11 @@ def load(path=None):
         "hbam_fixmate": (C.c_int, [vp, vp, vp, C.c_uint64, C.POINTER(FixmateRunC)]),
         "hbam_bgzf_compress": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_uint32, vp, C.c_int,
                                            C.c_uint64]),
+        "hbam_comm_unique_id": (C.c_int, [vp]),
+        "hbam_comm_init": (C.c_int, [vp, vp, C.c_int32, C.c_int32, C.POINTER(vp)]),
+        "hbam_comm_destroy": (None, [vp]),
+        "hbam_comm_split_points": (C.c_int, [vp, vp, C.POINTER(SortedRunC), C.c_uint32, vp]),
+        "hbam_sort_exchange": (C.c_int, [vp, vp, C.POINTER(SortedRunC), vp, C.POINTER(SortedRunC)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)
@@ -415,6 +428,26 @@ class Context:
                                    int(n_ref), int(window_bytes))
         if not s:
             raise HbamUnavailable("hbam_split_open failed: %s" % self.last_error())
+        return self._stream(s, host, keep)
+
+    def split_stream_reader(self, read, file_len, v_start, v_end, n_ref, window_bytes=1 << 30, host=True):
+        """Split-local streamed BAMRecordReader (hbam_split_open_reader): read(offset, length) ->
+        bytes is a positioned read of the file (os.pread, FSDataInputStream.read(long, ...)); only
+        the blocks the split needs are requested.  Yields as split_stream."""
+        def cb(user, off, n, dst):
+            b = read(int(off), int(n))
+            if not b:
+                return -1
+            C.memmove(dst, bytes(b), len(b))
+            return len(b)
+        fn = READ_FN(cb)
+        s = self.L.hbam_split_open_reader(self.h, fn, None, int(file_len), v_start, v_end, int(n_ref),
+                                          int(window_bytes))
+        if not s:
+            raise HbamUnavailable("hbam_split_open_reader failed: %s" % self.last_error())
+        return self._stream(s, host, fn)
+
+    def _stream(self, s, host, keep):
         try:
             while True:
                 d = Columns()
@@ -436,12 +469,14 @@ class Context:
         finally:
             self.last_stream_stats = self._split_stats(s)
             self.L.hbam_split_close(s)
+            del keep
 
     def _split_stats(self, s):
         b, w = C.c_uint64(0), C.c_uint64(0)
         ms = C.c_double(0)
         self.L.hbam_split_stats(s, C.byref(b), C.byref(ms), C.byref(w))
-        return {"h2d_bytes": int(b.value), "h2d_ms": float(ms.value), "windows": int(w.value)}
+        return {"h2d_bytes": int(b.value), "h2d_ms": float(ms.value), "windows": int(w.value),
+                "read_bytes": int(self.L.hbam_split_read_bytes(s))}
 
     def decode_split_device(self, data, v_start, v_end, n_ref, comp_base=0, file_len=None):
         """Device-resident decode (bench path): returns the hbam_columns struct."""

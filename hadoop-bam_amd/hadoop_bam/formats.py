@@ -842,8 +842,17 @@ class BAMRecordReader:
         if isinstance(h, int):
             raise_for(h, "cannot read SAM header")
         window = int(conf.get(WINDOW_BYTES_PROPERTY, 1 << 30))
-        self._gen = self.ctxt.split_stream(data, split.getStartVirtualOffset(),
-                                           split.getEndVirtualOffset(), h["n_ref"], window)
+        if isinstance(data, np.memmap):
+            # a file: split-local positioned reads (the reference seeks an FSDataInputStream,
+            # :128-143, WrapSeekable.java:42-87) — only the blocks the split needs are read
+            self._fd = os.open(path, os.O_RDONLY)
+            fd = self._fd
+            self._gen = self.ctxt.split_stream_reader(lambda off, n: os.pread(fd, n, off), len(data),
+                                                      split.getStartVirtualOffset(),
+                                                      split.getEndVirtualOffset(), h["n_ref"], window)
+        else:
+            self._gen = self.ctxt.split_stream(data, split.getStartVirtualOffset(),
+                                               split.getEndVirtualOffset(), h["n_ref"], window)
         self.dec = None
         self.i = self.n = 0
         self.status = 0
@@ -898,6 +907,9 @@ class BAMRecordReader:
             self._gen.close()
         self._gen = None
         self.dec = None
+        if getattr(self, "_fd", None) is not None:
+            os.close(self._fd)
+            self._fd = None
 
 
 # ---- input formats -------------------------------------------------------------------

@@ -13,9 +13,12 @@ MI355X design — one process per GPU, one exchange step:
   2. regular samples of the sorted local keys are all-gathered; the P-1 split points are their
      quantiles (deterministic, unlike the reference's unseeded RandomSampler — a partition
      choice never changes the concatenated order);
-  3. one all_to_all_single per column (keys, voffsets, block sizes, record bytes) over RCCL /
-     xGMI; every destination range is contiguous in the locally sorted order, so no packing
-     kernel is needed beyond step 1;
+  3. the exchange by key range: with an RcclComm (one GPU per rank) it is libhbam's own
+     hbam_sort_exchange — a count all-gather and one grouped ncclSend/ncclRecv of keys,
+     voffsets, block sizes and record bytes over xGMI, behind the C ABI a Java host binds too;
+     with a gloo group (CPU tests, ranks sharing one GPU) one all_to_all_single per column
+     staged through host memory.  Every destination range is contiguous in the locally sorted
+     order, so no packing kernel is needed beyond step 1;
   4. each rank stably sorts what it received (chunks arrive in source-rank order = file order),
      so the global order is (key, voffset) — the documented tie-break.
 
@@ -47,14 +50,67 @@ def _addr(p):
     return C.cast(p, C.c_void_p).value
 
 
-class HipSortOps:
-    """Product ops: every step is a libhbam call on the context's device and stream."""
+class RcclComm:
+    """libhbam's RCCL communicator (hbam_comm_init): one rank per GPU, the Sort exchange's
+    transport behind the C ABI (SURVEY.md §8(b) hbam_sort_multi_gpu).  Collective: every rank
+    constructs it with the same 128-byte unique id (rank 0's hbam_comm_unique_id)."""
 
-    def __init__(self, ctx):
+    ID_BYTES = 128
+
+    def __init__(self, ctx, nranks, rank, unique_id):
+        self.ctx = ctx
+        self.L = ctx.L
+        self.nranks, self.rank = int(nranks), int(rank)
+        uid = (C.c_uint8 * self.ID_BYTES).from_buffer_copy(bytes(unique_id))
+        self.h = C.c_void_p()
+        rc = self.L.hbam_comm_init(ctx.h, uid, self.nranks, self.rank, C.byref(self.h))
+        if rc:
+            raise RuntimeError("hbam_comm_init failed (%d): %s" % (rc, ctx.last_error()))
+
+    @staticmethod
+    def unique_id(L):
+        buf = (C.c_uint8 * RcclComm.ID_BYTES)()
+        rc = L.hbam_comm_unique_id(buf)
+        if rc:
+            raise RuntimeError("hbam_comm_unique_id failed (%d): RCCL unavailable" % rc)
+        return bytes(buf)
+
+    @classmethod
+    def from_dist(cls, ctx, dist):
+        """Rank 0's unique id broadcast over an initialised torch.distributed group."""
+        import torch
+        rank, world = dist.get_rank(), dist.get_world_size()
+        dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl"
+               else torch.device("cpu"))
+        t = torch.zeros(cls.ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            t.copy_(torch.frombuffer(bytearray(cls.unique_id(ctx.L)), dtype=torch.uint8))
+        dist.broadcast(t, 0)
+        return cls(ctx, world, rank, t.cpu().numpy().tobytes())
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            self.L.hbam_comm_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HipSortOps:
+    """Product ops: every step is a libhbam call on the context's device and stream.  With an
+    RcclComm the split points and the exchange are libhbam's too (hbam_comm_split_points,
+    hbam_sort_exchange)."""
+
+    def __init__(self, ctx, comm=None):
         import torch
         self.torch = torch
         self.ctx = ctx
         self.L = ctx.L
+        self.comm = comm
         self.dev = torch.device("cuda", torch.cuda.current_device())
 
     def _after_torch(self):
@@ -117,6 +173,33 @@ class HipSortOps:
             self.ctx.h, C.c_void_p(keys.data_ptr()), C.c_void_p(voffset.data_ptr()),
             C.c_void_p(block_size.data_ptr()), C.c_void_p(payload.data_ptr()), n, r), n)
 
+    @staticmethod
+    def _run_struct(run):
+        from ._lib import SortedRunC
+        return SortedRunC(run.n, int(run.offsets[-1].item()) if run.n else 0, run.keys.data_ptr(),
+                          run.voffset.data_ptr(), run.block_size.data_ptr(), run.offsets.data_ptr(),
+                          run.payload.data_ptr())
+
+    def split_points_native(self, run, samples_per_rank=4096):
+        """hbam_comm_split_points: regular samples of every rank's sorted keys all-gathered over
+        RCCL, their nranks-1 quantiles (choose_split_points' rule)."""
+        P = self.comm.nranks
+        sp = np.zeros(max(P - 1, 1), np.int64)
+        r = self._run_struct(run)
+        self._after_torch()
+        self._chk(self.L.hbam_comm_split_points(self.ctx.h, self.comm.h, C.byref(r), samples_per_rank,
+                                                C.c_void_p(sp.ctypes.data)), "hbam_comm_split_points")
+        return sp[:P - 1]
+
+    def exchange_native(self, run, split_points):
+        """hbam_sort_exchange: partition, count all-gather, grouped ncclSend/ncclRecv, re-sort."""
+        sp = np.ascontiguousarray(split_points, np.int64)
+        if len(sp) == 0:
+            sp = np.zeros(1, np.int64)
+        r = self._run_struct(run)
+        return self._run(lambda o: self.L.hbam_sort_exchange(self.ctx.h, self.comm.h, C.byref(r),
+                                                             C.c_void_p(sp.ctypes.data), o), run.n)
+
     def partition(self, run, split_points):
         """hbam_sort_partition: TotalOrderPartitioner record / byte bounds (host int64 arrays)."""
         from ._lib import SortedRunC
@@ -156,6 +239,8 @@ def exchange(run, split_points, dist, ops, stage_cpu=None):
     """all_to_all of a SortedRun by key range; returns this rank's globally-ordered run.
     Rank r receives the keys in (sp[r-1], sp[r]].  With a CPU-only backend (gloo) and device
     runs, the collective's buffers are staged through host memory (stage_cpu, default: gloo)."""
+    if getattr(ops, "comm", None) is not None:
+        return ops.exchange_native(run, split_points)
     import torch
     world = dist.get_world_size()
     dev = run.keys.device
@@ -199,6 +284,8 @@ def exchange(run, split_points, dist, ops, stage_cpu=None):
 
 def sort_sharded(run, dist, ops, all_gather_fn):
     """Steps 2-4 for one rank: split points, exchange, local stable sort."""
+    if getattr(ops, "comm", None) is not None:
+        return ops.exchange_native(run, ops.split_points_native(run))
     sp = choose_split_points(run.keys, dist.get_world_size(), all_gather_fn)
     return exchange(run, sp, dist, ops)
 

@@ -131,7 +131,7 @@ typedef struct hbam_timing {
   double scan_ms, inflate_ms, crc_ms, walk_ms, decode_ms, pools_ms, total_ms;
   double huffman_ms, resolve_ms; /* inflate = Huffman pass (k_inflate_tokens) + k_resolve (LZ77) */
   uint64_t n_blocks, comp_bytes, ubuf_bytes, n_records, pool_bytes;
-  uint64_t reserved;
+  double exchange_ms; /* hbam_sort_exchange: the grouped ncclSend/ncclRecv on the context stream */
 } hbam_timing;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -185,7 +185,8 @@ int hbam_decode_split(hbam_ctx* ctx, const uint8_t* comp, int on_device, uint64_
                       int32_t n_ref, hbam_columns* out);
 int hbam_columns_to_host(hbam_ctx* ctx, const hbam_columns* dev, hbam_columns* host);
 /* Streamed split read: BAMRecordReader over FileVirtualSplit
- * [v_start, v_end) of a file the caller holds in host memory (e.g. mmap), decoded in windows
+ * [v_start, v_end) of a file the caller holds in host memory (e.g. mmap; only the split's
+ * windows are copied, see hbam_split_open_reader for the bound), decoded in windows
  * of about window_bytes compressed bytes.  While window k decodes, the predicted window k+1
  * is copied to the device on a second HIP stream.  hbam_split_next fills `out` (device
  * columns, valid until the next call on the stream's context) with the next window's
@@ -196,9 +197,22 @@ typedef struct hbam_split_stream hbam_split_stream;
 hbam_split_stream* hbam_split_open(hbam_ctx* ctx, const uint8_t* file, uint64_t file_len,
                               uint64_t v_start, uint64_t v_end, int32_t n_ref,
                               uint64_t window_bytes);
+/* Split-local streamed read (BAMRecordReader.java:128-143 reads only the blocks the split touches,
+ * through FSDataInputStream.seek, util/WrapSeekable.java:42-87): the caller's read(user, offset,
+ * len, dst) fills dst with file bytes [offset, offset + len) and returns the bytes read (> 0; a
+ * positioned read such as FSDataInputStream.read(long, byte[], int, int) or pread).  Only bytes
+ * from v_start's block to a bound past v_end's block are read (at most (v_end >> 16) + 192 KiB
+ * unless a record runs longer), each at most once: the windows' overlap is re-used from the
+ * previous window's pinned staging.  Same output as hbam_split_open on the whole file.
+ * hbam_split_read_bytes: the bytes requested from `read` so far. */
+typedef int64_t (*hbam_read_fn)(void* user, uint64_t offset, uint64_t len, uint8_t* dst);
+hbam_split_stream* hbam_split_open_reader(hbam_ctx* ctx, hbam_read_fn read, void* user, uint64_t file_len,
+                                     uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                                     uint64_t window_bytes);
 int hbam_split_next(hbam_split_stream* s, hbam_columns* out);
 /* bytes copied host->device and the copies' wall time (ms) so far */
 int hbam_split_stats(const hbam_split_stream* s, uint64_t* h2d_bytes, double* h2d_ms, uint64_t* windows);
+uint64_t hbam_split_read_bytes(const hbam_split_stream* s);
 void hbam_split_close(hbam_split_stream* s);
 void hbam_free_host_columns(hbam_columns* host);
 void hbam_release_columns(hbam_ctx* ctx, hbam_columns* dev);
@@ -310,6 +324,33 @@ int hbam_merge_remap(hbam_ctx* ctx, hbam_columns* dv, const int32_t* ref_map, in
 int hbam_sort_received(hbam_ctx* ctx, const int64_t* key, const int64_t* voffset,
                        const int32_t* block_size, const uint8_t* payload, uint64_t n,
                        hbam_sorted_run* out);
+
+/* ---- Sort plugin exchange over RCCL (Sort.java:131-170: the TotalOrderPartitioner + Hadoop
+ * shuffle between map and reduce tasks; SURVEY.md §8(b) hbam_sort_multi_gpu, §8(e) steps 2-3).
+ * One rank per GPU.  RCCL (librccl.so.1) is loaded on the first hbam_comm_init.
+ *   rank 0: hbam_comm_unique_id(id); the job ships the 128 bytes to every rank (a Hadoop
+ *           Configuration property, MPI, torch.distributed.broadcast);
+ *   every rank, collectively: hbam_comm_init(ctx, id, nranks, rank, &comm);
+ *   every rank, collectively: hbam_comm_split_points(ctx, comm, run, samples, sp) — regular
+ *           samples of each rank's sorted keys all-gathered (ncclAllGather), the nranks-1 split
+ *           points their quantiles (deterministic; the reference's RandomSampler is unseeded);
+ *   every rank, collectively, twice: hbam_sort_exchange(ctx, comm, run, sp, out) — first with
+ *           out->payload == NULL: the partition of `run` (hbam_sort_partition) and the count
+ *           all-gather, out->n / out->payload_bytes = what this rank will receive; then with
+ *           caller-owned device buffers (as hbam_sort_split): one ncclGroupStart of per-peer
+ *           ncclSend / ncclRecv of keys, voffsets, block sizes and payload bytes (rank r gets
+ *           the keys in (sp[r-1], sp[r]]), then hbam_sort_received on what arrived (chunks in
+ *           source-rank order), so out is rank r's slice of the total order (key, file order).
+ * A communicator is tied to one context (its device and stream). */
+typedef struct hbam_comm hbam_comm;
+#define HBAM_UNIQUE_ID_BYTES 128
+int hbam_comm_unique_id(uint8_t* id_out);
+int hbam_comm_init(hbam_ctx* ctx, const uint8_t* id, int32_t nranks, int32_t rank, hbam_comm** out);
+void hbam_comm_destroy(hbam_comm* comm);
+int hbam_comm_split_points(hbam_ctx* ctx, hbam_comm* comm, const hbam_sorted_run* run,
+                           uint32_t samples_per_rank, int64_t* split_points);
+int hbam_sort_exchange(hbam_ctx* ctx, hbam_comm* comm, const hbam_sorted_run* run,
+                       const int64_t* split_points, hbam_sorted_run* out);
 
 /* SplittingBAMIndexer (SplittingBAMIndexer.java:146-248, §8 f-2) from a whole-file decode
  * (dv: device columns of hbam_decode_split over [first record, len<<16|0xffff]): out (host)

@@ -1,6 +1,6 @@
 // Drop-in body of SummarizeRecordReader (cli/plugins/chipster/Summarize.java:664-755) over the C
-// ABI (SURVEY.md §8 f-4).  The base reader is the BAM read path's split stream (hbam_split_open /
-// hbam_split_next, as HipBAMRecordReader); each window's records are cut into CIGAR ranges on the
+// ABI (SURVEY.md §8 f-4).  The base reader is the BAM read path's split stream
+// (hbam_split_open_reader / hbam_split_next over SplitSource, as HipBAMRecordReader); each window's records are cut into CIGAR ranges on the
 // device (hbam_summarize_ranges) and nextKeyValue() hands out (LongWritable key, Range) exactly in
 // the reference's order, raising its exception (the base reader's, IllegalArgumentException for a
 // CIGAR op code > 8, IndexOutOfBoundsException for a mapped record without a range) where it does.
@@ -26,6 +26,7 @@ import hbparquet.hadoop.util.ContextUtil;
 import org.seqdoop.hadoop_bam.FileVirtualSplit;
 import org.seqdoop.hadoop_bam.hip.Hbam;
 import org.seqdoop.hadoop_bam.hip.HipBAMRecordReader;
+import org.seqdoop.hadoop_bam.hip.SplitSource;
 import org.seqdoop.hadoop_bam.util.SAMHeaderReader;
 
 public class HipSummarizeRecordReader extends RecordReader<LongWritable, Range> {
@@ -33,6 +34,7 @@ public class HipSummarizeRecordReader extends RecordReader<LongWritable, Range> 
   private final Range value = new Range();
 
   private Hbam hbam;
+  private SplitSource source;
   private Arena arena, window;       // reader lifetime / the current window's host copies
   private MemorySegment stream, dev, ranges;
   private MemorySegment keys, begs, ends, revs;
@@ -51,17 +53,11 @@ public class HipSummarizeRecordReader extends RecordReader<LongWritable, Range> 
     }
     final long len = fs.getFileStatus(file).getLen();
     arena = Arena.ofShared();
-    final MemorySegment bytes = HipBAMRecordReader.mapFile(fs, file, len, arena);
     hbam = new Hbam(conf.getInt(HipBAMRecordReader.DEVICE_PROPERTY, 0), false);
-    try {
-      stream = (MemorySegment) Hbam.SPLIT_OPEN.invokeExact(hbam.context(), bytes, len,
-          split.getStartVirtualOffset(), split.getEndVirtualOffset(),
-          header.getSequenceDictionary().size(),
-          conf.getLong(HipBAMRecordReader.WINDOW_BYTES_PROPERTY, 1L << 30));
-    } catch (Throwable t) {
-      throw new IOException(t);
-    }
-    if (stream.address() == 0) throw new IOException("hbam_split_open: " + hbam.lastError());
+    source = new SplitSource(fs, file, arena);  // the split's bytes only (positioned reads)
+    stream = source.open(hbam, len, split.getStartVirtualOffset(), split.getEndVirtualOffset(),
+                         header.getSequenceDictionary().size(),
+                         conf.getLong(HipBAMRecordReader.WINDOW_BYTES_PROPERTY, 1L << 30));
     dev = arena.allocate(Hbam.COLUMNS);
     ranges = arena.allocate(Hbam.RANGES);
     n = i = 0;
@@ -123,10 +119,12 @@ public class HipSummarizeRecordReader extends RecordReader<LongWritable, Range> 
   @Override public void close() throws IOException {
     try {
       if (stream != null && stream.address() != 0) Hbam.SPLIT_CLOSE.invokeExact(stream);
+      if (source != null) source.close();
     } catch (Throwable t) {
       throw new IOException(t);
     } finally {
       stream = null;
+      source = null;
       if (window != null) window.close();
       window = null;
       if (hbam != null) hbam.close();

@@ -40,6 +40,10 @@ public final class Hbam implements AutoCloseable {
   static final MethodHandle SPLIT_OPEN = fn("hbam_split_open",
       FunctionDescriptor.of(A, A, A, J, J, J, I, J));
   static final MethodHandle SPLIT_NEXT = fn("hbam_split_next", FunctionDescriptor.of(I, A, A));
+  // split-local streamed read: positioned reads through an upcall stub (SplitSource)
+  static final MethodHandle SPLIT_OPEN_READER = fn("hbam_split_open_reader",
+      FunctionDescriptor.of(A, A, A, A, J, J, J, I, J));
+  static final MethodHandle SPLIT_READ_BYTES = fn("hbam_split_read_bytes", FunctionDescriptor.of(J, A));
   static final MethodHandle HOST_REGISTER = fn("hbam_host_register", FunctionDescriptor.of(I, A, A, J));
   static final MethodHandle HOST_UNREGISTER = fn("hbam_host_unregister", FunctionDescriptor.of(I, A, A));
   static final MethodHandle SPLIT_CLOSE = fn("hbam_split_close", FunctionDescriptor.ofVoid(A));
@@ -63,6 +67,12 @@ public final class Hbam implements AutoCloseable {
   static final MethodHandle SORT_PARTITION = fn("hbam_sort_partition", FunctionDescriptor.of(I, A, A, A, I, A, A));
   static final MethodHandle SORT_RECEIVED = fn("hbam_sort_received", FunctionDescriptor.of(I, A, A, A, A, A, J, A));
   static final MethodHandle MERGE_REMAP = fn("hbam_merge_remap", FunctionDescriptor.of(I, A, A, A, I, A));
+  // the exchange over RCCL (HipSort.Comm): Sort.java:131-170's partitioner + shuffle
+  static final MethodHandle COMM_UNIQUE_ID = fn("hbam_comm_unique_id", FunctionDescriptor.of(I, A));
+  static final MethodHandle COMM_INIT = fn("hbam_comm_init", FunctionDescriptor.of(I, A, A, I, I, A));
+  static final MethodHandle COMM_DESTROY = fn("hbam_comm_destroy", FunctionDescriptor.ofVoid(A));
+  static final MethodHandle COMM_SPLIT_POINTS = fn("hbam_comm_split_points", FunctionDescriptor.of(I, A, A, A, I, A));
+  static final MethodHandle SORT_EXCHANGE = fn("hbam_sort_exchange", FunctionDescriptor.of(I, A, A, A, A, A));
   static final MethodHandle SPLITS_WINDOWS = fn("hbam_probabilistic_splits_windows",
       FunctionDescriptor.of(J, A, A, J, A, I, A, J, A, A, J, A, A));
   // SURVEY.md §8 f-4: Summarize ranges, FixMate shuffle + reducer, device -> host copies

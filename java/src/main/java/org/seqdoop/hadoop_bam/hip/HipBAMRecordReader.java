@@ -1,7 +1,8 @@
 // Drop-in body of org.seqdoop.hadoop_bam.BAMRecordReader (BAMRecordReader.java:48-188) over
 // the C ABI.  initialize() reads the header as the reference does (:128-130) and opens a
-// streamed device decode of the FileVirtualSplit (hbam_split_open: windows of
-// hadoopbam.hip.window-bytes compressed bytes, the next copied while the current decodes);
+// streamed device decode of the FileVirtualSplit (hbam_split_open_reader: windows of
+// hadoopbam.hip.window-bytes compressed bytes, the next copied while the current decodes, each
+// read from the FSDataInputStream by positioned reads of the split's own bytes, SplitSource);
 // nextKeyValue() hands out (LongWritable key, SAMRecordWritable) from each window's host
 // columns and throws the reference's exception at the record where the reference would.
 // The value is the lazily decoded BAMRecord htsjdk would build from the same record bytes.
@@ -10,13 +11,10 @@ package org.seqdoop.hadoop_bam.hip;
 import java.io.ByteArrayInputStream;
 import java.io.IOException;
 import java.lang.foreign.*;
-import java.nio.channels.FileChannel;
-import java.nio.file.StandardOpenOption;
 
 import org.apache.hadoop.conf.Configuration;
 import org.apache.hadoop.fs.FSDataInputStream;
 import org.apache.hadoop.fs.FileSystem;
-import org.apache.hadoop.fs.LocalFileSystem;
 import org.apache.hadoop.fs.Path;
 import org.apache.hadoop.io.LongWritable;
 import org.apache.hadoop.mapreduce.InputSplit;
@@ -66,8 +64,8 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
   private BAMRecordCodec codec;
   private ValidationStringency stringency;
   private long fileStart, virtualEnd;
-  private int[] mergeMap;
-  private MemorySegment registered;  // the file bytes hbam_host_register locked  // HipSortRecordReader: merged index of each input index, or null
+  private int[] mergeMap;            // HipSortRecordReader: merged index of each input index, or null
+  private SplitSource source;        // positioned reads of the split's bytes (hbam_read_fn upcalls)
 
   /** Utils.correctSAMRecordForMerging on the device for every window (hbam_merge_remap):
    *  SortRecordReader (Sort.java:279-295) sets it when the inputs' dictionaries differ. */
@@ -96,53 +94,20 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     final long len = fs.getFileStatus(file).getLen();
 
     arena = Arena.ofShared();
-    final MemorySegment bytes = mapFile(fs, file, len, arena);
     hbam = new Hbam(conf.getInt(DEVICE_PROPERTY, 0), false);
-    // page-locked for the library's HIP runtime, so each window's copy overlaps the previous
-    // window's decode; a mapping the driver refuses to lock is still read (synchronously)
-    try {
-      registered = (int) Hbam.HOST_REGISTER.invokeExact(hbam.context(), bytes, len) == Hbam.OK ? bytes : null;
-    } catch (Throwable t) {
-      registered = null;
-    }
     fileStart = split.getStartVirtualOffset() >>> 16;
     virtualEnd = split.getEndVirtualOffset();
-    try {
-      stream = (MemorySegment) Hbam.SPLIT_OPEN.invokeExact(hbam.context(), bytes, len,
-          split.getStartVirtualOffset(), virtualEnd, nRef,
-          conf.getLong(WINDOW_BYTES_PROPERTY, 1L << 30));
-    } catch (Throwable t) {
-      throw new IOException(t);
-    }
-    if (stream.address() == 0) throw new IOException("hbam_split_open: " + hbam.lastError());
+    // only the split's blocks are read (into the library's pinned staging, so each window's copy
+    // overlaps the previous window's decode), as the reference's seek + read (:128-143)
+    source = new SplitSource(fs, file, arena);
+    stream = source.open(hbam, len, split.getStartVirtualOffset(), virtualEnd, nRef,
+                         conf.getLong(WINDOW_BYTES_PROPERTY, 1L << 30));
     dev = arena.allocate(Hbam.COLUMNS);
     host = arena.allocate(Hbam.COLUMNS);
     n = i = 0;
     status = Hbam.OK;
     last = false;
     nextWindow();
-  }
-
-  /** The file's bytes as one segment: mmap for the local file system, else read off-heap. */
-  public static MemorySegment mapFile(FileSystem fs, Path file, long len, Arena arena)
-      throws IOException {
-    if (fs instanceof LocalFileSystem || "file".equals(fs.getUri().getScheme())) {
-      try (FileChannel ch = FileChannel.open(java.nio.file.Path.of(file.toUri()),
-                                             StandardOpenOption.READ)) {
-        return ch.map(FileChannel.MapMode.READ_ONLY, 0, len, arena);
-      }
-    }
-    final MemorySegment seg = arena.allocate(Math.max(len, 1), 16);
-    final byte[] chunk = new byte[1 << 22];
-    try (FSDataInputStream in = fs.open(file)) {
-      for (long off = 0; off < len; ) {
-        final int k = in.read(off, chunk, 0, (int) Math.min(chunk.length, len - off));
-        if (k < 0) throw new IOException("short read of " + file);
-        MemorySegment.copy(chunk, 0, seg, ValueLayout.JAVA_BYTE, off, k);
-        off += k;
-      }
-    }
-    return seg;
   }
 
   private static MemorySegment ptr(MemorySegment cols, String f, long bytes) {
@@ -155,7 +120,10 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     try {
       if (hostLive) { Hbam.FREE_HOST.invokeExact(host); hostLive = false; }
       final int rc = (int) Hbam.SPLIT_NEXT.invokeExact(stream, dev);
-      if (rc < 0) throw new RuntimeIOException("hbam_split_next: " + hbam.lastError());
+      if (rc < 0) {
+        if (source.failure() != null) throw new RuntimeIOException(source.failure());
+        throw new RuntimeIOException("hbam_split_next: " + hbam.lastError());
+      }
       if (rc == 0) { last = true; n = i = 0; return false; }
       if (mergeMap != null) {
         try (Arena a = Arena.ofConfined()) {
@@ -227,13 +195,13 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     try {
       if (hostLive) Hbam.FREE_HOST.invokeExact(host);
       if (stream != null && stream.address() != 0) Hbam.SPLIT_CLOSE.invokeExact(stream);
-      if (registered != null) { final int rc = (int) Hbam.HOST_UNREGISTER.invokeExact(hbam.context(), registered); }
+      if (source != null) source.close();
     } catch (Throwable t) {
       throw new IOException(t);
     } finally {
       hostLive = false;
       stream = null;
-      registered = null;
+      source = null;
       if (hbam != null) hbam.close();
       hbam = null;
       if (arena != null) arena.close();

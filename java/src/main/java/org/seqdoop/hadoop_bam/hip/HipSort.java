@@ -2,8 +2,11 @@
 // a node's decoded splits sorted on the GPU (hbam_sort_split: stable radix by the signed
 // LongWritable key, the record bytes gathered in key order), cut at the TotalOrderPartitioner's
 // split points (hbam_sort_partition: each partition's record and byte range, contiguous), and
-// after the caller's transport of the partitions (MPI, an RCCL all-to-all, a Hadoop shuffle)
-// the received concatenation sorted stably again (hbam_sort_received).  Ties keep input order,
+// after the transport of the partitions the received concatenation sorted stably again
+// (hbam_sort_received).  The transport between the GPUs of a node is libhbam's own RCCL
+// exchange (Comm: hbam_comm_init, hbam_comm_split_points, hbam_sort_exchange — one rank per
+// GPU, grouped ncclSend/ncclRecv over xGMI); a host with another transport (MPI, a Hadoop
+// shuffle) uses partition() + received() around it instead.  Ties keep input order,
 // so the output is ordered by (key, input, voffset): the documented tie-break.  Device buffers
 // are hbam_device_alloc'ed and owned by the returned Run.
 package org.seqdoop.hadoop_bam.hip;
@@ -102,6 +105,72 @@ public final class HipSort {
       throw e;
     } catch (Throwable t) {
       throw new IOException(t);
+    }
+  }
+
+  /** One rank of the node's RCCL exchange (hbam_comm_*).  Rank 0 calls uniqueId(); the job ships
+   *  the 128 bytes to every rank (e.g. a Configuration property, base64); every rank then
+   *  constructs its Comm collectively on the context of its GPU. */
+  public static final class Comm implements AutoCloseable {
+    public static final int ID_BYTES = 128;
+    private final Hbam hbam;
+    private final MemorySegment comm;
+    public final int nranks, rank;
+
+    public static byte[] uniqueId() throws IOException {
+      try (Arena a = Arena.ofConfined()) {
+        final MemorySegment id = a.allocate(ID_BYTES);
+        final int rc = (int) Hbam.COMM_UNIQUE_ID.invokeExact(id);
+        if (rc != Hbam.OK) throw new IOException("hbam_comm_unique_id: RCCL unavailable (" + rc + ")");
+        return id.toArray(ValueLayout.JAVA_BYTE);
+      } catch (IOException e) {
+        throw e;
+      } catch (Throwable t) {
+        throw new IOException(t);
+      }
+    }
+
+    public Comm(Hbam h, byte[] uniqueId, int nranks, int rank) throws IOException {
+      this.hbam = h;
+      this.nranks = nranks;
+      this.rank = rank;
+      try (Arena a = Arena.ofConfined()) {
+        final MemorySegment id = a.allocateFrom(ValueLayout.JAVA_BYTE, uniqueId);
+        final MemorySegment out = a.allocate(A);
+        final int rc = (int) Hbam.COMM_INIT.invokeExact(h.context(), id, nranks, rank, out);
+        if (rc != Hbam.OK) throw new IOException("hbam_comm_init: " + h.lastError());
+        comm = out.get(A, 0);
+      } catch (IOException e) {
+        throw e;
+      } catch (Throwable t) {
+        throw new IOException(t);
+      }
+    }
+
+    /** The TotalOrderPartitioner's nranks-1 split points from every rank's sorted run (collective;
+     *  the stand-in for InputSampler.writePartitionFile, Sort.java:154-157). */
+    public long[] splitPoints(Run run, int samplesPerRank) throws IOException {
+      try (Arena a = Arena.ofConfined()) {
+        final MemorySegment sp = a.allocate(J, Math.max(nranks - 1, 1));
+        final int rc = (int) Hbam.COMM_SPLIT_POINTS.invokeExact(hbam.context(), comm, run.struct, samplesPerRank, sp);
+        if (rc != Hbam.OK) throw new IOException("hbam_comm_split_points: " + hbam.lastError());
+        return java.util.Arrays.copyOf(sp.toArray(J), nranks - 1);
+      } catch (IOException e) {
+        throw e;
+      } catch (Throwable t) {
+        throw new IOException(t);
+      }
+    }
+
+    /** This rank's slice of the total order: the partitions of every rank's run exchanged by key
+     *  range and sorted again (collective). */
+    public Run exchange(Run local, long[] splitPoints, Arena arena) throws IOException {
+      final MemorySegment sp = arena.allocateFrom(J, splitPoints.length == 0 ? new long[] {0} : splitPoints);
+      return run(hbam, r -> (int) Hbam.SORT_EXCHANGE.invokeExact(hbam.context(), comm, local.struct, sp, r), arena);
+    }
+
+    @Override public void close() {
+      try { Hbam.COMM_DESTROY.invokeExact(comm); } catch (Throwable t) { throw new RuntimeException(t); }
     }
   }
 

@@ -107,6 +107,8 @@ def _ctype_letter(t):
     if "*" in t:
         return "A"
     t = t.replace("const", "").strip()
+    if t == "hbam_read_fn":  # a function pointer (the Java shim's upcall stub)
+        return "A"
     if t in ("int", "int32_t", "uint32_t"):
         return "I"
     if t in ("int64_t", "uint64_t", "size_t"):

@@ -643,9 +643,33 @@ def test_resolve_forged_descriptor_is_an_error_not_a_hang(gpu_ctx, case):
 
 
 # ---- config #4 shape: byte-range shards read through streamed windows ------------------------
-def _stream_read(gpu_ctx, data, a, z, n_ref, window):
-    """hbam_split_open/next over one FileVirtualSplit -> (concatenated columns, n windows)."""
-    ws = list(gpu_ctx.split_stream(data, int(a), int(z), n_ref, window_bytes=window))
+class _CountingReader:
+    """A positioned read over a byte array that records every byte range requested (the
+    FSDataInputStream.read(long, byte[], int, int) a Java map task would hand in)."""
+
+    def __init__(self, data):
+        self.data = data
+        self.ranges = []
+
+    def __call__(self, off, n):
+        self.ranges.append((off, n))
+        return self.data[off:off + n].tobytes()
+
+    def total(self):
+        return sum(n for _, n in self.ranges)
+
+    def overlaps(self):
+        r = sorted(self.ranges)
+        return sum(max(0, (a0 + n0) - a1) for (a0, n0), (a1, _) in zip(r, r[1:]))
+
+
+def _stream_read(gpu_ctx, data, a, z, n_ref, window, reader=None):
+    """hbam_split_open/next (or hbam_split_open_reader/next with `reader`) over one
+    FileVirtualSplit -> (concatenated columns, n windows)."""
+    if reader is not None:
+        ws = list(gpu_ctx.split_stream_reader(reader, len(data), int(a), int(z), n_ref, window_bytes=window))
+    else:
+        ws = list(gpu_ctx.split_stream(data, int(a), int(z), n_ref, window_bytes=window))
     cat = {"n": sum(w["n"] for w in ws), "status": 0, "err_record": 0}
     base = 0
     for w in ws:
@@ -664,11 +688,14 @@ def _stream_read(gpu_ctx, data, a, z, n_ref, window):
 
 @pytest.mark.parametrize("name", GOLDEN_FILES)
 @pytest.mark.parametrize("P", [2, 3, 5])
-def test_sharded_split_windows_match_oracle(gpu_ctx, oracle_mod, name, P):
+@pytest.mark.parametrize("split_local", [False, True])
+def test_sharded_split_windows_match_oracle(gpu_ctx, oracle_mod, name, P, split_local):
     """P byte-range FileSplits of one file, aligned by the guesser (addProbabilisticSplits),
     each read through 64 KiB streamed windows (EMORE continuation at every window end): every
     shard equals the oracle's BAMRecordReader for that FileVirtualSplit, record bytes included;
-    without the duplicated boundary-block records the shards concatenate to the whole-file read."""
+    without the duplicated boundary-block records the shards concatenate to the whole-file read.
+    split_local: the same through hbam_split_open_reader (positioned reads of the split's bytes
+    only, each byte requested once)."""
     data = _load(name)
     L = len(data)
     b = np.array([L * k // P for k in range(P)], np.uint64)
@@ -683,8 +710,15 @@ def test_sharded_split_windows_match_oracle(gpu_ctx, oracle_mod, name, P):
     shards, windows = [], 0
     for a, z in zip(vs, ve):
         ref = oracle_mod.read_split(data, int(a), int(z))
-        got, nwin = _stream_read(gpu_ctx, data, a, z, h["n_ref"], 64 << 10)
+        rd = _CountingReader(data) if split_local else None
+        got, nwin = _stream_read(gpu_ctx, data, a, z, h["n_ref"], 64 << 10, reader=rd)
         assert_same_split(got, ref)
+        if rd is not None:
+            # only [vStart's block, vEnd's block + 192 KiB), no byte twice (the windows' overlap
+            # is re-used from the previous window's staging)
+            assert rd.overlaps() == 0
+            assert min(o for o, _ in rd.ranges) >= int(a) >> 16
+            assert max(o + n for o, n in rd.ranges) <= min(L, (int(z) >> 16) + (3 << 16))
         assert got["payload"] == oracle_mod.record_payloads(ref)[0].tobytes()
         windows += nwin
         shards.append(got)
@@ -697,6 +731,30 @@ def test_sharded_split_windows_match_oracle(gpu_ctx, oracle_mod, name, P):
             cut = int(np.searchsorted(sh["voffset"], vo[-1], side="right")) if vo else 0
             vo.extend(sh["voffset"][cut:])
         assert np.array_equal(np.array(vo, np.uint64), whole["voffset"])
+
+
+def test_split_local_reader_reads_the_split_not_the_file(gpu_ctx, oracle_mod):
+    """A small FileVirtualSplit of a 24 MB file through hbam_split_open_reader: the records equal
+    the oracle's, and the bytes requested stay within the split's compressed bytes plus one
+    window plus 64 KiB (BAMRecordReader.java:128-143 seeks; HipBAMRecordReader no longer copies
+    the whole file for a non-local file system)."""
+    import genbam
+    data = np.asarray(genbam.generate(target_bytes=24 << 20, seed=11))
+    h = oracle_mod.read_header(data)
+    L = len(data)
+    for beg, size, window in ((L // 3, 1 << 20, 1 << 20), (L // 2, 4 << 20, 256 << 10), (L - (2 << 20), 2 << 20, 1 << 20)):
+        end = min(L, beg + size)
+        vs, ve = oracle_mod.probabilistic_splits(data, np.array([beg], np.uint64), np.array([end], np.uint64))
+        a, z = int(vs[0]), int(ve[0])
+        ref = oracle_mod.read_split(data, a, z)
+        rd = _CountingReader(data)
+        got, nwin = _stream_read(gpu_ctx, data, a, z, h["n_ref"], window, reader=rd)
+        assert_same_split(got, ref)
+        assert got["payload"] == oracle_mod.record_payloads(ref)[0].tobytes()
+        split_bytes = (z >> 16) - (a >> 16)
+        assert rd.overlaps() == 0
+        assert rd.total() <= split_bytes + window + (64 << 10), (rd.total(), split_bytes)
+        assert rd.total() < L // 4
 
 
 def test_windowed_decode_comp_base(gpu_ctx, oracle_mod):

@@ -247,6 +247,59 @@ def test_two_process_gpu_sort_matches_total_order(oracle_mod, fname):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fname", ["edge_unsorted_l1.bam", "small_pe.bam", "edge_uniform_long.bam"])
+def test_rccl_exchange_one_rank_matches_oracle(gpu_ctx, oracle_mod, fname):
+    """The exchange behind the C ABI (hbam_comm_init + hbam_comm_split_points +
+    hbam_sort_exchange) on a one-rank RCCL communicator: the count all-gather and the grouped
+    ncclSend/ncclRecv (to itself) of keys, voffsets, block sizes and payload, then the re-sort,
+    equal the oracle's total order, payload bytes included.  (A box has one GPU; RCCL refuses two
+    ranks on one device, so N > 1 runs only on the driver's 8-GPU node.)"""
+    import torch
+    from hadoop_bam import sort
+    data = np.fromfile(os.path.join(GOLDEN, fname), dtype=np.uint8)
+    want_k, want_v, want_p, want_off, cols = _oracle_sorted(data)
+    d = torch.from_numpy(data).cuda()
+    h = gpu_ctx.parse_header(d)
+    rc, dc = gpu_ctx.decode_split_device(d, h["first_voffset"], (len(data) << 16) | 0xffff, h["n_ref"])
+    assert rc == 0 and dc.status == 0
+    comm = sort.RcclComm(gpu_ctx, 1, 0, sort.RcclComm.unique_id(gpu_ctx.L))
+    try:
+        ops = sort.HipSortOps(gpu_ctx, comm)
+        # a run in FILE order (not key order), so the re-sort after the exchange does the work
+        n = int(dc.n_records)
+        pay, off = oracle_mod.record_payloads(cols)
+        run = sort.SortedRun(torch.from_numpy(cols["key"].astype(np.int64)).cuda(),
+                             torch.from_numpy(cols["voffset"].astype(np.int64)).cuda(),
+                             torch.from_numpy(cols["block_size"].astype(np.int32)).cuda(),
+                             torch.from_numpy(pay).cuda(), torch.from_numpy(off.astype(np.int64)).cuda())
+        assert run.n == n
+        sp = ops.split_points_native(run)
+        assert len(sp) == 0
+        out = ops.exchange_native(run, sp)
+        assert gpu_ctx.timing()["exchange_ms"] > 0
+        assert out.n == n
+        assert np.array_equal(out.keys.cpu().numpy(), want_k)
+        assert np.array_equal(out.voffset.cpu().numpy(), want_v)
+        assert np.array_equal(out.offsets.cpu().numpy(), want_off)
+        assert out.payload.cpu().numpy().tobytes() == want_p.tobytes()
+        # sort_sharded drives the same native path when the ops carry a communicator
+        out2 = sort.sort_sharded(ops.run_from_columns(dc), None, ops, None)
+        assert np.array_equal(out2.keys.cpu().numpy(), want_k)
+        assert out2.payload.cpu().numpy().tobytes() == want_p.tobytes()
+        # the exchange proper without its size query is refused
+        from hadoop_bam._lib import SortedRunC
+        import ctypes as C
+        r = ops._run_struct(run)
+        o = SortedRunC(out.n, int(out.offsets[-1]), out.keys.data_ptr(), out.voffset.data_ptr(),
+                       out.block_size.data_ptr(), out.offsets.data_ptr(), out.payload.data_ptr())
+        z = np.zeros(1, np.int64)
+        assert gpu_ctx.L.hbam_sort_exchange(gpu_ctx.h, comm.h, C.byref(r), C.c_void_p(z.ctypes.data),
+                                            C.byref(o)) == -11
+    finally:
+        comm.close()
+
+
+@pytest.mark.gpu
 def test_sort_received_after_async_device_op(gpu_ctx, oracle_mod):
     """sort_received's inputs produced by asynchronous torch work (pinned non_blocking copies
     and kernels still queued on torch's stream) must be complete before libhbam's own stream

@@ -1,6 +1,6 @@
 """Config #5 benchmark: coordinate Sort plugin path on an unsorted synthetic BAM.
 
-Per rank (one process per GPU; torchrun for N > 1, RCCL all_to_all): decode the rank's shard
+Per rank (one process per GPU; torchrun for N > 1, hbam_sort_exchange over RCCL): decode the rank's shard
 (hbam_decode_split, compressed bytes resident in HBM), key-sort it on the device
 (hbam_sort_keys + hbam_permute + hbam_gather_records), then — N > 1 — split points,
 all_to_all by key range and the local stable re-sort (hadoop_bam/sort.py).  Prints one JSON
@@ -44,7 +44,8 @@ def main():
     d = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
     d[:len(data)].copy_(torch.from_numpy(data))
     ctx = _lib.Context(local)
-    ops = sort.HipSortOps(ctx)
+    # N > 1: the exchange is libhbam's own (hbam_sort_exchange over an RCCL communicator)
+    ops = sort.HipSortOps(ctx, sort.RcclComm.from_dist(ctx, dist) if dist else None)
     h = ctx.parse_header(d[:len(data)])
     ag = parallel.torch_all_gather_fn(dist, "cuda") if dist else None
 
@@ -111,7 +112,7 @@ def main():
                       "achieved_GBps": round(alg / (sort_ms / 1e3) / 1e9, 1) if sort_ms else None},
             "config": {"workload": "config#5 per GPU: unsorted synthetic 150bp PE BAM, decode + "
                                    "getKey + device radix sort + record pack%s" %
-                                   (" + RCCL all_to_all by key range" if world > 1 else ""),
+                                   (" + hbam_sort_exchange (RCCL grouped send/recv) by key range" if world > 1 else ""),
                        "compressed_bytes_per_gpu": len(data)},
         }), flush=True)
     if dist:

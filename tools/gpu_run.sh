@@ -1,0 +1,58 @@
+#!/bin/bash
+# One parameterised GPU call (replaces the per-call gpu_r3*.sh scripts of round 3):
+#   gpurun -- bash tools/gpu_run.sh OUT STEP[,ARG...] ...
+# Steps run in order, each under its own time limit, and the first one that fails hard (a
+# fault, an abort, a time limit) ends the call; pytest's "some tests failed" (rc 1) does not.
+#   tests[,EXPR]         pytest -m gpu (optionally -k EXPR)
+#   smoke                __graft_entry__.smoke()
+#   bench[,STEPS]        python bench.py (default --steps 20 --warmup 3)
+#   prof                 rocprofv3 --kernel-trace --stats of a short bench.py run
+#   pmc,COUNTERS         one rocprofv3 --pmc pass (COUNTERS separated by '+') of a short run
+#   abdecode,SIZE,LIBS   tools/ab_decode.py A/B of library builds (LIBS separated by '+')
+#   stream,SIZE,WINDOW   tools/bench_stream.py (config #4 share)
+#   sort,SIZE            tools/bench_sort.py (config #5 share)
+#   guess,SIZE           tools/bench_guess.py (config #3)
+#   crc                  tools/check_inflate_crc.py
+#   py,SCRIPT[,ARGS..]   any repo script (ARGS separated by ',')
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/$1
+shift
+mkdir -p $O
+export TMPDIR=/tmp
+hard() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
+for spec in "$@"; do
+  IFS=, read -r step a1 a2 a3 <<< "$spec"
+  echo "== $spec $(date +%T)" >> $O/steps.log
+  case $step in
+    tests)
+      K=(); [ -n "$a1" ] && K=(-k "$a1")
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread "${K[@]}" > $O/tests.txt 2>&1; r=$? ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1; r=$? ;;
+    bench)
+      timeout -k 10 600 python -u bench.py --steps ${a1:-20} --warmup 3 > $O/bench.json 2> $O/bench.err; r=$? ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --parity-splits 0 > $O/bench_prof.json 2> $O/prof.err; r=$? ;;
+    pmc)
+      timeout -s KILL 300 rocprofv3 --pmc ${a1//+/ } -d $O/pmc_${a1//+/_} -o run -- python3 tools/ab_decode.py --size ${a2:-2e9} --reps 1 --libs libhbam.so > $O/pmc_${a1//+/_}.txt 2>&1; r=$? ;;
+    abdecode)
+      timeout -k 10 900 python -u tools/ab_decode.py --size ${a1:-5e9} --reps ${a3:-3} --libs ${a2//+/ } > $O/ab_${a2//+/_}.txt 2>&1; r=$? ;;
+    stream)
+      timeout -k 10 600 python -u tools/bench_stream.py --size ${a1:-25e9} --window ${a2:-2e9} --reps 2 > $O/stream.json 2> $O/stream.err; r=$? ;;
+    sort)
+      timeout -k 10 600 python -u tools/bench_sort.py --size ${a1:-12.5e9} > $O/sort.json 2> $O/sort.err; r=$? ;;
+    guess)
+      timeout -k 10 700 python -u tools/bench_guess.py --size ${a1:-50e9} --guesses 10000 --check 10000 > $O/guess.json 2> $O/guess.err; r=$? ;;
+    crc)
+      timeout -k 10 900 python -u tools/check_inflate_crc.py > $O/crc.txt 2>&1; r=$? ;;
+    py)
+      IFS=, read -r -a ARGS <<< "${spec#py,$a1}"
+      timeout -k 10 900 python -u "$a1" "${ARGS[@]}" > $O/$(basename $a1 .py).txt 2>&1; r=$? ;;
+    *)
+      echo "unknown step $spec" >> $O/steps.log; r=2 ;;
+  esac
+  echo "rc $r $(date +%T)" >> $O/steps.log
+  if hard $r; then exit 0; fi
+done
+exit 0
