@@ -1190,6 +1190,7 @@ struct hbam_split_stream {
   void* user = nullptr;
   uint8_t* hbuf[2] = {nullptr, nullptr};
   uint64_t hcap[2] = {0, 0};
+  uint64_t hbase[2] = {0, 0}, hlen[2] = {0, 0};  // file bytes each staging slot holds
   uint64_t read_bytes = 0;  // bytes requested from the callback
   uint8_t* dbuf[2] = {nullptr, nullptr};
   uint64_t dcap[2] = {0, 0};
@@ -1228,34 +1229,82 @@ uint64_t split_limit(uint64_t v_end, uint64_t file_len) {
   return e >= file_len || file_len - e <= SPLIT_TAIL ? file_len : e + SPLIT_TAIL;
 }
 
-// read-callback streams: file bytes [b, b + n) into host staging slot k — the part the other
-// slot's staging already holds (the windows' overlap) is copied from there, the rest read once
+// read-callback streams: file bytes [b, b + n) into host staging slot k.  Whatever either slot's
+// staging already holds (the windows' overlap, a window re-copied at a resume point) is copied
+// from there — slot k's own bytes first, by one memmove, before anything else lands in its
+// buffer — and only the rest is asked of the callback, so every file byte is read once.
 int stream_stage(hbam_split_stream* s, int k, uint64_t b, uint64_t n) {
   hbam_ctx* c = s->c;
+  const uint64_t e = b + n;
+  uint8_t* dst = s->hbuf[k];
+  uint8_t* fresh = nullptr;
   if (s->hcap[k] < n + 64) {
-    if (s->hbuf[k]) HIPCHK(c, hipHostFree(s->hbuf[k]));
-    s->hbuf[k] = nullptr;
-    s->hcap[k] = 0;
-    if (hipHostMalloc((void**)&s->hbuf[k], n + 64, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void**)&fresh, n + 64, hipHostMallocDefault) != hipSuccess) {
       (void)hipGetLastError();
       return set_err(c, HBAM_ENOMEM, "hbam_split_next: hipHostMalloc(%llu) failed", (unsigned long long)(n + 64));
     }
+    dst = fresh;
+  }
+  // covered[] = the new range's bytes already in place, as [lo, hi) file intervals
+  uint64_t cov_lo[2] = {0, 0}, cov_hi[2] = {0, 0};
+  int ncov = 0;
+  auto take = [&](int src) {
+    if (!s->hbuf[src] || !s->hlen[src]) return;
+    const uint64_t lo = std::max(b, s->hbase[src]), hi = std::min(e, s->hbase[src] + s->hlen[src]);
+    if (lo >= hi) return;
+    memmove(dst + (lo - b), s->hbuf[src] + (lo - s->hbase[src]), hi - lo);
+    cov_lo[ncov] = lo;
+    cov_hi[ncov] = hi;
+    ++ncov;
+  };
+  take(k);  // own bytes first (in place: a single memmove)
+  // the other slot's, outside what slot k supplied
+  if (s->hbuf[1 - k] && s->hlen[1 - k]) {
+    const int o = 1 - k;
+    uint64_t lo = std::max(b, s->hbase[o]), hi = std::min(e, s->hbase[o] + s->hlen[o]);
+    if (ncov && lo < hi) {  // clip to the part not covered yet (k's cover is one interval)
+      if (lo >= cov_lo[0] && hi <= cov_hi[0]) lo = hi;
+      else if (lo >= cov_lo[0] && lo < cov_hi[0]) lo = cov_hi[0];
+      else if (hi > cov_lo[0] && hi <= cov_hi[0]) hi = cov_lo[0];
+    }
+    if (lo < hi) {
+      memcpy(dst + (lo - b), s->hbuf[o] + (lo - s->hbase[o]), hi - lo);
+      cov_lo[ncov] = lo;
+      cov_hi[ncov] = hi;
+      ++ncov;
+    }
+  }
+  // the gaps, from the callback
+  uint64_t p = b;
+  while (p < e) {
+    bool moved = false;
+    for (int q = 0; q < ncov; ++q)
+      if (p >= cov_lo[q] && p < cov_hi[q]) {
+        p = cov_hi[q];
+        moved = true;
+      }
+    if (moved) continue;
+    uint64_t stop = e;
+    for (int q = 0; q < ncov; ++q)
+      if (cov_lo[q] > p) stop = std::min(stop, cov_lo[q]);
+    while (p < stop) {
+      const int64_t got = s->read(s->user, p, stop - p, dst + (p - b));
+      if (got <= 0) {
+        if (fresh) (void)hipHostFree(fresh);
+        return set_err(c, HBAM_EIO, "hbam_split_next: read(%llu, %llu) returned %lld", (unsigned long long)p,
+                       (unsigned long long)(stop - p), (long long)got);
+      }
+      s->read_bytes += std::min<uint64_t>((uint64_t)got, stop - p);
+      p += std::min<uint64_t>((uint64_t)got, stop - p);
+    }
+  }
+  if (fresh) {
+    if (s->hbuf[k]) HIPCHK(c, hipHostFree(s->hbuf[k]));
+    s->hbuf[k] = fresh;
     s->hcap[k] = n + 64;
   }
-  uint64_t have = 0;
-  const int o = 1 - k;
-  if (s->valid[o] && s->hbuf[o] && s->base[o] <= b && b < s->base[o] + s->len[o]) {
-    have = std::min(n, s->base[o] + s->len[o] - b);
-    memcpy(s->hbuf[k], s->hbuf[o] + (b - s->base[o]), have);
-  }
-  while (have < n) {
-    const int64_t got = s->read(s->user, b + have, n - have, s->hbuf[k] + have);
-    if (got <= 0)
-      return set_err(c, HBAM_EIO, "hbam_split_next: read(%llu, %llu) returned %lld", (unsigned long long)(b + have),
-                     (unsigned long long)(n - have), (long long)got);
-    s->read_bytes += (uint64_t)got;
-    have += std::min<uint64_t>((uint64_t)got, n - have);
-  }
+  s->hbase[k] = b;
+  s->hlen[k] = n;
   return HBAM_OK;
 }
 

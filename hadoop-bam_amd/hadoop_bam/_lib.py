@@ -478,6 +478,29 @@ class Context:
         return {"h2d_bytes": int(b.value), "h2d_ms": float(ms.value), "windows": int(w.value),
                 "read_bytes": int(self.L.hbam_split_read_bytes(s))}
 
+    def download(self, ptr, nbytes, dtype=np.uint8):
+        """hbam_download: `nbytes` of device memory at address `ptr` -> numpy array of dtype."""
+        a = np.empty(max(int(nbytes), 1), np.uint8)
+        if nbytes:
+            rc = self.L.hbam_download(self.h, C.c_void_p(int(ptr)), int(nbytes), C.c_void_p(a.ctypes.data))
+            if rc:
+                raise RuntimeError("hbam_download failed (%d): %s" % (rc, self.last_error()))
+        return a[:int(nbytes)].view(dtype)
+
+    def columns_slice(self, d, i0, i1):
+        """Host copy of records [i0, i1) of device columns `d` (an hbam_decode_split /
+        hbam_split_next result): the fixed columns and each record's SAMRecordWritable bytes."""
+        n = max(0, int(i1) - int(i0))
+        out = {"n": n}
+        for name, dt in FIXED:
+            sz = np.dtype(dt).itemsize
+            p = C.cast(getattr(d, name), C.c_void_p).value
+            out[name] = self.download(p + int(i0) * sz, n * sz, dt).copy() if n else np.zeros(0, dt)
+        ub = C.cast(d.ubuf, C.c_void_p).value
+        out["records"] = [self.download(ub + int(o), 4 + int(b)).tobytes()
+                          for o, b in zip(out["rec_off"], out["block_size"])]
+        return out
+
     def decode_split_device(self, data, v_start, v_end, n_ref, comp_base=0, file_len=None):
         """Device-resident decode (bench path): returns the hbam_columns struct."""
         p, n, dev, keep = self._ptr(data)

@@ -14,7 +14,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "hadoop-bam_amd"), os.path.join(ROOT, "tools")]
+sys.path[:0] = [os.path.join(ROOT, "hadoop-bam_amd"), os.path.join(ROOT, "tools"), os.path.join(ROOT, "oracle")]
 import numpy as np  # noqa: E402
 
 
@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--parity", type=int, default=1)
+    ap.add_argument("--oracle-splits", type=int, default=32)
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -84,6 +86,9 @@ def main():
     # sanity: the output is sorted by key and covers every decoded record
     k = run.keys
     assert bool((k[1:] >= k[:-1]).all()) if run.n > 1 else True
+    parity = None
+    if a.parity and not dist:
+        parity = sort_parity(ctx, ops, d[:len(data)], data, h, run, a)
     tot = torch.tensor([el, float(n_dec), float(run.n), ub], dtype=torch.float64, device="cuda")
     if dist:
         mx = tot.clone()
@@ -110,6 +115,7 @@ def main():
                          "exchange_resort": round(float(m[2]), 4)},
             "radix": {"ms": round(sort_ms, 3), "passes": passes, "records": n_dec,
                       "achieved_GBps": round(alg / (sort_ms / 1e3) / 1e9, 1) if sort_ms else None},
+            "parity": parity,
             "config": {"workload": "config#5 per GPU: unsorted synthetic 150bp PE BAM, decode + "
                                    "getKey + device radix sort + record pack%s" %
                                    (" + hbam_sort_exchange (RCCL grouped send/recv) by key range" if world > 1 else ""),
@@ -117,6 +123,80 @@ def main():
         }), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def sort_parity(ctx, ops, dev, data, h, run, a):
+    """The timed run's output at size (SortReducer's output order, Sort.java:191-205): ordered by
+    (key, voffset) (the documented tie-break), its voffsets a permutation of the decoded split's,
+    every payload the decoded record's bytes (re-gathered from the decode by voffset, compared on
+    the device in chunks); then --oracle-splits random 32 MiB FileSplits decoded and sorted on the
+    device against the oracle's read_split + sort order, payload bytes included."""
+    import ctypes as C
+    import torch
+    import oracle
+    t = time.time()
+    n = run.n
+    k, v = run.keys, run.voffset
+    order_ok = bool(((k[1:] > k[:-1]) | ((k[1:] == k[:-1]) & (v[1:] > v[:-1]))).all()) if n > 1 else True
+    # the decoded split again (the context's buffers): its voffsets in file order
+    rc, cols = ctx.decode_split_device(dev, h["first_voffset"], (len(data) << 16) | 0xffff, h["n_ref"])
+    assert rc == 0 and cols.status == 0
+    m = int(cols.n_records)
+    ident = torch.arange(m, dtype=torch.int32, device="cuda")
+    dv = torch.empty(m, dtype=torch.int64, device="cuda")
+    assert ctx.L.hbam_permute(ctx.h, C.cast(cols.voffset, C.c_void_p), 8, C.c_void_p(ident.data_ptr()), m,
+                              C.c_void_p(dv.data_ptr())) == 0
+    del ident
+    j = torch.searchsorted(dv, v)
+    perm_ok = m == n and bool((j < m).all()) and bool((dv[j.clamp(max=m - 1)] == v).all())
+    if perm_ok:
+        seen = torch.zeros(m, dtype=torch.int8, device="cuda")
+        seen[j] = 1
+        perm_ok = bool(seen.all())
+        del seen
+    pay_bad = 0
+    if perm_ok:
+        jp = j.to(torch.int32)
+        chunk = 1 << 22
+        for c0 in range(0, n, chunk):
+            c1 = min(n, c0 + chunk)
+            lo, hi = int(run.offsets[c0]), int(run.offsets[c1])
+            exp = torch.empty(hi - lo + 64, dtype=torch.uint8, device="cuda")
+            off = torch.empty(c1 - c0 + 1, dtype=torch.int64, device="cuda")
+            tot = C.c_uint64(0)
+            assert ctx.L.hbam_gather_records(ctx.h, C.cast(cols.ubuf, C.c_void_p), C.cast(cols.rec_off, C.c_void_p),
+                                             C.cast(cols.block_size, C.c_void_p), C.c_void_p(jp.data_ptr() + 4 * c0),
+                                             c1 - c0, C.c_void_p(exp.data_ptr()), hi - lo + 64,
+                                             C.c_void_p(off.data_ptr()), C.byref(tot)) == 0
+            if int(tot.value) != hi - lo or not torch.equal(exp[:hi - lo], run.payload[lo:hi]):
+                pay_bad += 1
+    # oracle sample: random 32 MiB FileSplits, device decode + sort vs the oracle
+    rng = np.random.default_rng(a.seed + 77)
+    span = len(data) - (48 << 20)
+    o_bad, o_recs = 0, 0
+    host = np.ascontiguousarray(data)
+    for beg in (np.sort(rng.integers(0, span, a.oracle_splits)) if span > 0 else []):
+        end = int(beg) + (32 << 20)
+        vs, ve = oracle.probabilistic_splits(host, np.array([beg], np.uint64), np.array([end], np.uint64))
+        rc, dc = ctx.decode_split_device(dev, int(vs[0]), int(ve[0]), h["n_ref"])
+        ref = oracle.read_split(host, int(vs[0]), int(ve[0]))
+        pay, offs = oracle.record_payloads(ref)
+        o = oracle.sort_order(ref["key"])
+        noff, npay = oracle._regather(pay, offs, o)
+        sr = ops.run_from_columns(dc)
+        same = rc == 0 and sr.n == ref["n"] and np.array_equal(sr.keys.cpu().numpy(), ref["key"][o]) and \
+            np.array_equal(sr.voffset.cpu().numpy(), ref["voffset"].astype(np.int64)[o]) and \
+            sr.payload.cpu().numpy().tobytes() == npay.tobytes()
+        o_bad += 0 if same else 1
+        o_recs += ref["n"]
+    return {"order_key_voffset": order_ok, "voffsets_permutation_of_decode": perm_ok,
+            "payload_chunks_bad": pay_bad, "records": n,
+            "oracle_splits": a.oracle_splits, "oracle_records": o_recs, "oracle_mismatches": o_bad,
+            "mismatches": (0 if order_ok else 1) + (0 if perm_ok else 1) + pay_bad + o_bad,
+            "seconds": round(time.time() - t, 1),
+            "what": "whole timed output: (key, voffset) order, voffsets a permutation of the decoded "
+                    "split's, every payload == the decoded record's bytes; plus random 32 MiB splits "
+                    "sorted on the device == the oracle's order and payloads"}
 
 
 if __name__ == "__main__":

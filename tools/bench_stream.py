@@ -2,8 +2,10 @@
 streamed reader (hbam_split_open/next: windows of --window compressed bytes, the next window
 copied H2D on a second stream while the current one decodes).  The rate is PCIe-inclusive
 (host bytes in, device columns out); it is the rate a map task reading a host-resident file
-sees, never bench.py's device-resident `value`.  Parity: the windows' records equal one
-device-resident decode of the same split (count, keys, voffsets).  Prints one JSON line."""
+sees, never bench.py's device-resident `value`.  Parity (--parity, outside the timed runs): the
+windows' records equal one device-resident decode of the same split — every voffset and key, and
+for the 64 records on each side of every window cut (where the EMORE continuation resumes)
+every fixed column and the record bytes.  Prints one JSON line per window size."""
 import argparse
 import ctypes as C
 import json
@@ -23,6 +25,7 @@ def main():
                     help="window sizes (compressed bytes); one JSON line each")
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--parity", type=int, default=1, help="check the windows against a resident decode")
     a = ap.parse_args()
     import torch
     import genbam
@@ -47,8 +50,67 @@ def main():
     rc, blocks = ctx.scan_blocks(host[:n])
     assert rc == 0
     U = int(np.sum(blocks["isize"].astype(np.uint64)))  # the file's inflated bytes
-    for win in a.window:
-        one_window_size(a, ctx, host, n, nrec, h, v0, v1, U, int(win))
+    lines = [one_window_size(a, ctx, host, n, nrec, h, v0, v1, U, int(win)) for win in a.window]
+    if a.parity:
+        ctx.close()  # its window-sized work buffers; the check decodes the whole file resident
+        par = stream_parity(host, n, h, v0, v1, int(a.window[-1]))
+        lines[-1]["parity"] = par
+    for ln in lines:
+        print(json.dumps(ln), flush=True)
+    if not all(ln["record_count_matches_generator"] for ln in lines) or \
+            (a.parity and lines[-1]["parity"]["mismatches"] != 0):
+        sys.exit(1)
+
+
+def _vp(p):
+    return C.cast(p, C.c_void_p).value
+
+
+def stream_parity(host, n, h, v0, v1, win):
+    """The streamed read of [v0, v1) in windows of `win` against one resident decode of the same
+    bytes: every voffset / key, and every fixed column + record bytes of the 64 records on each
+    side of each window cut."""
+    import torch
+    from hadoop_bam import _lib
+    t = time.time()
+    cs = _lib.Context(0)
+    vo, ky, sl = [], [], []
+    base = 0
+    for d in cs.split_stream(host[:n], v0, v1, h["n_ref"], window_bytes=win, host=False):
+        m = int(d.n_records)
+        vo.append(cs.download(_vp(d.voffset), 8 * m, np.uint64).copy())
+        ky.append(cs.download(_vp(d.key), 8 * m, np.int64).copy())
+        sl.append((base, cs.columns_slice(d, 0, min(64, m))))
+        sl.append((base + max(0, m - 64), cs.columns_slice(d, max(0, m - 64), m)))
+        base += m
+    cs.close()
+    svo, sky = np.concatenate(vo), np.concatenate(ky)
+    del vo, ky
+    cr = _lib.Context(0)
+    dev = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    dev[n:].zero_()
+    dev[:n].copy_(torch.from_numpy(host[:n]))
+    rc, d = cr.decode_split_device(dev[:n], v0, v1, h["n_ref"])
+    assert rc == 0 and int(d.status) == 0, (rc, cr.last_error())
+    R = int(d.n_records)
+    mism = 0 if R == base else 1
+    rvo = cr.download(_vp(d.voffset), 8 * R, np.uint64)
+    rky = cr.download(_vp(d.key), 8 * R, np.int64)
+    mism += 0 if (R == base and np.array_equal(rvo, svo) and np.array_equal(rky, sky)) else 1
+    checked, bad = 0, 0
+    for start, got in sl:
+        ref = cr.columns_slice(d, start, start + got["n"])
+        same = all(np.array_equal(got[k], ref[k]) for k, _ in _lib.FIXED if k != "rec_off")
+        same = same and got["records"] == ref["records"]
+        checked += got["n"]
+        bad += 0 if same else 1
+    cr.close()
+    return {"records": base, "resident_records": R, "windows": len(sl) // 2,
+            "boundary_records_checked": checked, "boundary_slices_bad": bad,
+            "mismatches": mism + bad, "seconds": round(time.time() - t, 1),
+            "what": "every voffset and key of the streamed windows == one resident decode of the file; "
+                    "the 64 records on each side of every window cut: every fixed column and the "
+                    "record bytes"}
 
 
 def one_window_size(a, ctx, host, n, nrec, h, v0, v1, U, win):
@@ -75,7 +137,7 @@ def one_window_size(a, ctx, host, n, nrec, h, v0, v1, U, win):
                                                      st["h2d_ms"], marks), file=sys.stderr, flush=True)
     dt, recs, ub, wins, st, marks = min(reps, key=lambda x: x[0])
     ok = recs == nrec
-    print(json.dumps({
+    return ({
         "metric": "streamed split decode, PCIe-inclusive (config#4 shape, one MI355X)",
         "value": round(U / dt / 1e9, 3), "unit": "GB/s uncompressed", "uncompressed_bytes": U,
         "inflated_incl_window_overlap": ub, "records_per_s": round(recs / dt, 1),
@@ -84,9 +146,7 @@ def one_window_size(a, ctx, host, n, nrec, h, v0, v1, U, win):
         "per_window_host_s_and_decode_ms": marks,
         "h2d": {"bytes": st["h2d_bytes"], "ms": round(st["h2d_ms"], 2),
                 "gb_s": round(st["h2d_bytes"] / max(st["h2d_ms"], 1e-9) / 1e6, 2)},
-        "host_buffer": "page-locked for libhbam (hbam_host_register)", "record_count_matches_generator": ok}), flush=True)
-    if not ok:
-        sys.exit(1)
+        "host_buffer": "page-locked for libhbam (hbam_host_register)", "record_count_matches_generator": ok})
 
 
 if __name__ == "__main__":
