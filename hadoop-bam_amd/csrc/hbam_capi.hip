@@ -167,6 +167,14 @@ enum BufId {
   B_X_PAY,
   B_X_CNT,
   B_X_SAMP,
+  // multi-input Sort: read-/program-group rewrite (hbam_groups.hip)
+  B_G_TAB,
+  B_G_LENS,
+  B_G_ERR,
+  B_G_CODES,
+  B_G_OOFF,
+  B_G_BS,
+  B_G_PAY,
   B_COUNT_ALL
 };
 
@@ -2377,5 +2385,6 @@ extern "C" int64_t hbam_bgzf_compress(hbam_ctx* c, const uint8_t* src, int src_o
 }
 
 #include "hbam_consumers.hip"
+#include "hbam_groups.hip"
 #include "hbam_bcf_api.hip"
 #include "hbam_comm.hip"

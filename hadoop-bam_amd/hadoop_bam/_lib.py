@@ -29,6 +29,8 @@ HBAM_EMORE = -12
 HBAM_EINDEX = -13
 HBAM_ETRIBBLE = -14
 HBAM_ERUNTIME = -15
+HBAM_ENULL = -16
+HBAM_ECLASSCAST = -17
 
 CODE_NAMES = {
     HBAM_OK: "OK", HBAM_EIO: "IOException", HBAM_ETRUNC: "FileTruncatedException",
@@ -38,6 +40,7 @@ CODE_NAMES = {
     HBAM_EUNSUPPORTED: "Unsupported", HBAM_EDEVICE: "DeviceError", HBAM_EINVAL: "InvalidArgument",
     HBAM_EMORE: "NeedMoreData", HBAM_EINDEX: "IndexOutOfBoundsException",
     HBAM_ETRIBBLE: "TribbleException", HBAM_ERUNTIME: "RuntimeException",
+    HBAM_ENULL: "NullPointerException", HBAM_ECLASSCAST: "ClassCastException",
 }
 
 # every entry point include/hbam.h declares (checked by tests/test_abi.py)
@@ -57,7 +60,7 @@ EXPORTS = [
     "hbam_host_register", "hbam_host_unregister", "hbam_bcf_parse_header", "hbam_guess_bcf_window_len",
     "hbam_guess_bcf_windows", "hbam_bcf_decode_split", "hbam_comm_unique_id", "hbam_comm_init",
     "hbam_comm_destroy", "hbam_comm_split_points", "hbam_sort_exchange", "hbam_split_open_reader",
-    "hbam_split_read_bytes",
+    "hbam_split_read_bytes", "hbam_rewrite_groups",
 ]
 
 # hbam_read_fn: int64_t read(void* user, uint64_t offset, uint64_t len, uint8_t* dst)
@@ -218,6 +221,7 @@ def load(path=None):
         "hbam_split_open_reader": (vp, [vp, READ_FN, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int32,
                                         C.c_uint64]),
         "hbam_split_read_bytes": (C.c_uint64, [vp]),
+        "hbam_rewrite_groups": (C.c_int, [vp, C.POINTER(Columns), vp, C.c_uint64, _i32p, C.POINTER(C.c_uint64)]),
         "hbam_split_stats": (C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_double),
                                        C.POINTER(C.c_uint64)]),
         "hbam_split_close": (None, [vp]),

@@ -42,11 +42,20 @@ class JavaRuntimeException(RuntimeError):
     """RuntimeException wrapping java.util.zip.DataFormatException."""
 
 
+class NullPointerException(RuntimeError):
+    pass
+
+
+class ClassCastException(TypeError):
+    pass
+
+
 _EXC = {
     _lib.HBAM_EIO: IOException, _lib.HBAM_ETRUNC: FileTruncatedException,
     _lib.HBAM_EFORMAT: SAMFormatException, _lib.HBAM_ERUNTIMEIO: RuntimeIOException,
     _lib.HBAM_EEOF: RuntimeEOFException, _lib.HBAM_EREFID: IllegalArgumentException,
-    _lib.HBAM_EDATA: JavaRuntimeException,
+    _lib.HBAM_EDATA: JavaRuntimeException, _lib.HBAM_ENULL: NullPointerException,
+    _lib.HBAM_ECLASSCAST: ClassCastException,
 }
 
 

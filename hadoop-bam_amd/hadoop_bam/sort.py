@@ -296,14 +296,103 @@ class SAMException(RuntimeError):
 
 
 def _header_records(text, tag):
-    """(ID, attribute set) of every @RG / @PG line of a header text, in order."""
+    """(ID, [(tag, value), ...] without ID) of every @RG / @PG line of a header text, in order."""
     out = []
     for ln in text.split(b"\n"):
         if ln.startswith(tag + b"\t"):
-            f = ln.split(b"\t")[1:]
-            rid = next((x[3:] for x in f if x.startswith(b"ID:")), b"")
-            out.append((rid, frozenset(x for x in f if not x.startswith(b"ID:"))))
+            attrs = [(f[:2], f[3:]) for f in ln.split(b"\t")[1:] if len(f) >= 3]
+            rid = next((v for k, v in attrs if k == b"ID"), b"")
+            out.append((rid, [(k, v) for k, v in attrs if k != b"ID"]))
     return out
+
+
+def _rec_key(attrs):
+    """AbstractSAMHeaderRecord equality: the attribute map (last value of a repeated tag)."""
+    return frozenset(dict(attrs).items())
+
+
+def merge_header_records(records, taken, table, out):
+    """SamFileHeaderMerger.mergeHeaderRecords (htsjdk 1.131, restated, parity unpinned).
+    records: [(input index, ID, attrs)] in input order.  Records with one ID are grouped by their
+    attributes in first-seen order; the first distinct record of an ID keeps it (unless an earlier
+    round took it), every further one gets ID.1, ID.2 ... (the first free suffix).  table[input]
+    maps each input's original ID -> merged ID; out receives (merged ID, attrs).  -> collisions?"""
+    by_id = {}
+    for h, rid, attrs in records:
+        by_id.setdefault(rid, {}).setdefault(_rec_key(attrs), (attrs, []))[1].append(h)
+    collided = False
+    for rid, variants in by_id.items():
+        for attrs, heads in variants.values():
+            if rid not in taken:
+                new = rid
+            else:
+                collided = True
+                k = 1
+                while rid + b"." + str(k).encode() in taken:
+                    k += 1
+                new = rid + b"." + str(k).encode()
+            taken.add(new)
+            for h in heads:
+                table.setdefault(h, {})[rid] = new
+            out.append((new, attrs))
+    return collided
+
+
+def _no_duplicate_ids(headers, tag):
+    for h in headers:
+        ids = [rid for rid, _ in _header_records(h.text, tag)]
+        if len(ids) != len(set(ids)):
+            raise SAMException("Input file contains more than one %s with the same id"
+                               % tag.decode().lstrip("@"))
+
+
+def merge_read_groups(headers):
+    """mergeReadGroups: -> (collisions?, {input: {old: new}}, [(ID, attrs)] sorted by ID)."""
+    _no_duplicate_ids(headers, b"@RG")
+    recs = [(h, rid, attrs) for h, hd in enumerate(headers) for rid, attrs in _header_records(hd.text, b"@RG")]
+    table, out = {}, []
+    col = merge_header_records(recs, set(), table, out)
+    return col, table, sorted(out, key=lambda r: r[0])
+
+
+def merge_program_groups(headers):
+    """mergeProgramGroups: the PP (previous program) chains merged root first — the records
+    without PP, then each round the records whose PP names a record of the same input merged in
+    the round before — IDs and PPs translated between rounds.  -> (collisions?, {input: {old:
+    new}} (no entry for an input without @PG), [(ID, attrs)] sorted by ID)."""
+    _no_duplicate_ids(headers, b"@PG")
+    left = [[h, rid, list(attrs)] for h, hd in enumerate(headers) for rid, attrs in _header_records(hd.text, b"@PG")]
+    pp = lambda attrs: next((v for k, v in attrs if k == b"PP"), None)
+    cur = [r for r in left if pp(r[2]) is None]
+    left = [r for r in left if pp(r[2]) is not None]
+    taken, table, result, col = set(), {}, [], False
+    while cur:
+        out = []
+        col |= merge_header_records([(h, rid, a) for h, rid, a in cur], taken, table, out)
+        result += out
+
+        def tr(rs, pp_too):
+            res = []
+            for h, rid, attrs in rs:
+                t = table.get(h, {})
+                nid = t.get(rid, rid)
+                a = attrs
+                if pp_too and pp(attrs) is not None and t.get(pp(attrs)) not in (None, pp(attrs)):
+                    a = [(k, t[v] if k == b"PP" else v) for k, v in attrs]
+                res.append([h, nid, a])
+            return res
+        cur = tr(cur, False)
+        left = tr(left, True)
+        nxt, rest = [], []
+        for r in left:
+            if any(r[0] == c[0] and pp(r[2]) == c[1] for c in cur):
+                nxt.append(r)
+            else:
+                rest.append(r)
+        left, cur = rest, nxt
+    if left:
+        raise SAMException("%d program groups weren't processed. Do their PP ids point to existing PGs?" % len(left))
+    return col, table, sorted(result, key=lambda r: r[0])
 
 
 def merge_sequences(into, frm):
@@ -341,14 +430,11 @@ class SamFileHeaderMerger:
     """new SamFileHeaderMerger(sortOrder, headers, true) as Utils.getSAMHeaderMerger builds it
     (cli/Utils.java:252-283).  htsjdk 1.131 is absent here, so its behaviour is restated (parity
     unpinned): the dictionary is merged only when the inputs' dictionaries differ
-    (hasMergedSequenceDictionary), by mergeSequences over the inputs in order; the merged header
-    holds the merged dictionary, the inputs' @RG / @PG records (identical records from several
-    inputs kept once) and comments, sort order `sort_order`.
-
-    Read / program group ID collisions (one ID with different attributes in two inputs) are not
-    supported: correctSAMRecordForMerging then rewrites RG tags through the PROGRAM-group table
-    (Utils.java:318-323, getProgramGroupId for RG), which drops or NPEs in htsjdk; this raises
-    NotImplementedError instead of imitating that."""
+    (hasMergedSequenceDictionary), by mergeSequences over the inputs in order; read groups and
+    program groups by mergeReadGroups / mergeProgramGroups (an ID carried by records with different
+    attributes is renamed ID.1, ID.2, ...: hasReadGroupCollisions / hasProgramGroupCollisions, with
+    per-input translation tables); the merged header holds the merged dictionary, the merged @RG and
+    @PG records (sorted by ID) and the comments, sort order `sort_order`."""
 
     def __init__(self, sort_order, headers):
         self.headers = list(headers)
@@ -365,33 +451,47 @@ class SamFileHeaderMerger:
         names = {n: i for i, (n, _) in enumerate(self.merged_refs)}
         # createSequenceMapping: input index -> merged index, by name
         self.ref_maps = [np.array([names[n] for n, _ in d], np.int32) for d in dicts]
-        for tag in (b"@RG", b"@PG"):
-            seen = {}
-            for h in self.headers:
-                for rid, attrs in _header_records(h.text, tag):
-                    if seen.setdefault(rid, attrs) != attrs:
-                        raise NotImplementedError(
-                            "%s ID %r differs between inputs: the reference remaps RG tags through the "
-                            "program-group table (cli/Utils.java:314-323); not supported"
-                            % (tag.decode(), rid))
+        self.has_read_group_collisions, self.rg_tables, self.merged_rg = merge_read_groups(self.headers)
+        self.has_program_group_collisions, self.pg_tables, self.merged_pg = merge_program_groups(self.headers)
         self.sort_order = sort_order
+
+    def getProgramGroupId(self, input_index, original):
+        """samProgramGroupIdTranslation.get(header).get(id): NullPointerException when the input
+        has no @PG record (no table), None when the id is not one of its program groups."""
+        t = self.pg_tables.get(input_index)
+        if t is None:
+            from .formats import NullPointerException
+            raise NullPointerException("no program-group table for input %d" % input_index)
+        return t.get(original)
+
+    def getReadGroupId(self, input_index, original):
+        return self.rg_tables.get(input_index, {}).get(original)
+
+    def group_table(self, input_index):
+        """hbam_rewrite_groups' table for one input: what correctSAMRecordForMerging does to its
+        PG and RG tags (cli/Utils.java:314-324; both looked up in the PROGRAM-group table)."""
+        import struct
+        t = self.pg_tables.get(input_index)
+        out = b""
+        for collides in (self.has_program_group_collisions, self.has_read_group_collisions):
+            if not collides:
+                out += struct.pack("<BH", 0, 0)
+            elif t is None:
+                out += struct.pack("<BH", 2, 0)
+            else:
+                out += struct.pack("<BH", 1, len(t))
+                for old, new in t.items():
+                    out += struct.pack("<H", len(old)) + old + struct.pack("<h", len(new)) + new
+        return out
 
     def getMergedHeader(self):
         from .output import SAMFileHeader
         lines = [b"@HD\tVN:1.4\tSO:" + self.sort_order.encode()]
         for n, ln in self.merged_refs:
             lines.append(b"@SQ\tSN:" + n + b"\tLN:" + str(ln).encode())
-        for tag in (b"@RG", b"@PG"):
-            done = set()
-            recs = []
-            for h in self.headers:
-                for ln in h.text.split(b"\n"):
-                    if ln.startswith(tag + b"\t") and ln not in done:
-                        done.add(ln)
-                        recs.append(ln)
-            if tag == b"@RG":  # mergeReadGroups sorts by ID
-                recs.sort(key=lambda x: next((f[3:] for f in x.split(b"\t") if f.startswith(b"ID:")), b""))
-            lines += recs
+        for tag, recs in ((b"@RG", self.merged_rg), (b"@PG", self.merged_pg)):
+            for rid, attrs in recs:
+                lines.append(b"\t".join([tag, b"ID:" + rid] + [k + b":" + v for k, v in attrs]))
         for h in self.headers:
             lines += [ln for ln in h.text.split(b"\n") if ln.startswith(b"@CO")]
         return SAMFileHeader(b"\n".join(lines) + b"\n", self.merged_refs)
@@ -410,6 +510,24 @@ def correct_for_merging(ctx, cols, merger, input_index):
     if bad.value != (1 << 64) - 1:
         raise ValueError("Reference index not found in sequence dictionary (record %d of input %d: "
                          "SAMRecord.setReferenceIndex against the input's header)" % (bad.value, input_index))
+
+
+def correct_groups(ctx, cols, merger, input_index):
+    """correctSAMRecordForMerging's program-group / read-group rewrite (cli/Utils.java:314-324)
+    over a decoded split of input `input_index` (hbam_rewrite_groups: cols then points at the
+    rewritten records).  Raises the reference's exception at the first record that raises it."""
+    if not (merger.has_program_group_collisions or merger.has_read_group_collisions):
+        return
+    tab = merger.group_table(input_index)
+    buf = np.frombuffer(tab, np.uint8)
+    st, er = C.c_int32(0), C.c_uint64(0)
+    rc = ctx.L.hbam_rewrite_groups(ctx.h, C.byref(cols), C.c_void_p(buf.ctypes.data), len(buf), C.byref(st),
+                                   C.byref(er))
+    if rc:
+        raise RuntimeError("hbam_rewrite_groups failed (%d): %s" % (rc, ctx.last_error()))
+    if st.value:
+        from .formats import raise_for
+        raise_for(st.value, "record %d of input %d (correctSAMRecordForMerging)" % (er.value, input_index))
 
 
 def sort_inputs(ctx, inputs, ops=None, sort_order="coordinate"):
@@ -433,6 +551,7 @@ def sort_inputs(ctx, inputs, ops=None, sort_order="coordinate"):
         if rc or cols.status:
             raise RuntimeError("decode of input %d failed rc=%d status=%d: %s" % (i, rc, cols.status, ctx.last_error()))
         correct_for_merging(ctx, cols, merger, i)
+        correct_groups(ctx, cols, merger, i)
         runs.append(ops.run_from_columns(cols))
     if len(runs) == 1:
         return merger.getMergedHeader(), runs[0]

@@ -17,6 +17,8 @@
  *   HBAM_EINDEX       IndexOutOfBoundsException
  *   HBAM_ETRIBBLE     htsjdk TribbleException (BCF)
  *   HBAM_ERUNTIME     another RuntimeException out of BCF2Codec.decode (BCF, unpinned)
+ *   HBAM_ENULL        NullPointerException (multi-input Sort's group rewrite, cli/Utils.java:316-323)
+ *   HBAM_ECLASSCAST   ClassCastException (an RG / PG attribute that is not a string)
  *
  * Library-specific codes (no reference counterpart): HBAM_ENOMEM, HBAM_EUNSUPPORTED
  * (BGZF block with ISIZE > 65536), HBAM_EDEVICE (HIP error), HBAM_EINVAL, HBAM_EMORE
@@ -57,6 +59,8 @@ extern "C" {
 #define HBAM_EINDEX (-13) /* IndexOutOfBoundsException (Summarize.java:715 on a record without a range) */
 #define HBAM_ETRIBBLE (-14) /* htsjdk TribbleException (BCF2Codec: unreadable / inconsistent BCF record) */
 #define HBAM_ERUNTIME (-15) /* another RuntimeException escaping BCF2Codec.decode (restated, unpinned) */
+#define HBAM_ENULL (-16) /* NullPointerException (cli/Utils.java:316-323: a group lookup without a table) */
+#define HBAM_ECLASSCAST (-17) /* ClassCastException ((String) of a non-string RG / PG attribute) */
 
 typedef struct hbam_ctx hbam_ctx;
 
@@ -319,6 +323,22 @@ int hbam_sort_partition(hbam_ctx* ctx, const hbam_sorted_run* run, const int64_t
  * throws IllegalArgumentException there), else UINT64_MAX.  Run it before hbam_sort_split. */
 int hbam_merge_remap(hbam_ctx* ctx, hbam_columns* dv, const int32_t* ref_map, int32_t n_in,
                      uint64_t* bad_record);
+/* Multi-input Sort, continued: Utils.correctSAMRecordForMerging's program-group / read-group
+ * rewrite (cli/Utils.java:314-324) when SamFileHeaderMerger reports ID collisions.  Over a decoded
+ * split of input h (dv, after hbam_merge_remap): every record carrying the tag gets
+ * setAttribute(tag, getProgramGroupId(h, value)) — for RG too (the reference's quirk: RG values are
+ * looked up in the PROGRAM-group table) — and is re-encoded as BAMRecordCodec.encode writes a record
+ * whose attributes changed (integer tags re-typed, odd sequence pad nibble zeroed, absent qualities
+ * 0xFF, bin 0 when unplaced; restated from htsjdk 1.131, parity unpinned).  `table` (host) holds, for
+ * PG then RG: u8 mode (0 no collisions of that kind: untouched; 1 translate; 2 h has no @PG record:
+ * NullPointerException at the first record carrying the tag), u16 count, then `count` entries
+ * {u16 old_len, old bytes, i16 new_len (-1: the value is not in the table -> tag removed; not needed:
+ * an absent value is removed too), new bytes}.  On return dv's ubuf / ubuf_len / rec_off / block_size
+ * point at the rewritten records (context-owned; the aux pool is not refreshed) and *status is HBAM_OK,
+ * or the exception raised at record *err_record (HBAM_ENULL, HBAM_ECLASSCAST, HBAM_EFORMAT): dv then
+ * holds the records before it. */
+int hbam_rewrite_groups(hbam_ctx* ctx, hbam_columns* dv, const uint8_t* table, uint64_t table_len,
+                        int32_t* status, uint64_t* err_record);
 /* receive side: n records (device key/voffset/block_size and their packed payload, chunks in
  * source-rank order) as a sorted run */
 int hbam_sort_received(hbam_ctx* ctx, const int64_t* key, const int64_t* voffset,

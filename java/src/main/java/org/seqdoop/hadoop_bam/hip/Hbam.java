@@ -15,7 +15,8 @@ import htsjdk.samtools.util.RuntimeIOException;
 
 public final class Hbam implements AutoCloseable {
   public static final int OK = 0, EIO = -1, ETRUNC = -2, EFORMAT = -3, ERUNTIMEIO = -4,
-      EEOF = -5, EREFID = -6, EDATA = -7, EMORE = -12, EINDEX = -13, ETRIBBLE = -14, ERUNTIME = -15;
+      EEOF = -5, EREFID = -6, EDATA = -7, EMORE = -12, EINDEX = -13, ETRIBBLE = -14, ERUNTIME = -15,
+      ENULL = -16, ECLASSCAST = -17;
 
   private static final Linker LINKER = Linker.nativeLinker();
   private static final SymbolLookup LIB = SymbolLookup.libraryLookup(
@@ -67,6 +68,7 @@ public final class Hbam implements AutoCloseable {
   static final MethodHandle SORT_PARTITION = fn("hbam_sort_partition", FunctionDescriptor.of(I, A, A, A, I, A, A));
   static final MethodHandle SORT_RECEIVED = fn("hbam_sort_received", FunctionDescriptor.of(I, A, A, A, A, A, J, A));
   static final MethodHandle MERGE_REMAP = fn("hbam_merge_remap", FunctionDescriptor.of(I, A, A, A, I, A));
+  static final MethodHandle REWRITE_GROUPS = fn("hbam_rewrite_groups", FunctionDescriptor.of(I, A, A, A, J, A, A));
   // the exchange over RCCL (HipSort.Comm): Sort.java:131-170's partitioner + shuffle
   static final MethodHandle COMM_UNIQUE_ID = fn("hbam_comm_unique_id", FunctionDescriptor.of(I, A));
   static final MethodHandle COMM_INIT = fn("hbam_comm_init", FunctionDescriptor.of(I, A, A, I, I, A));
@@ -153,6 +155,8 @@ public final class Hbam implements AutoCloseable {
       case EINDEX: return new IndexOutOfBoundsException(where);
       case ETRIBBLE: return new htsjdk.tribble.TribbleException(where);
       case ERUNTIME: return new RuntimeException("BCF2Codec.decode: " + where);
+      case ENULL: return new NullPointerException(where);
+      case ECLASSCAST: return new ClassCastException(where);
       default: return new RuntimeIOException("hbam error " + code + " at " + where);
     }
   }

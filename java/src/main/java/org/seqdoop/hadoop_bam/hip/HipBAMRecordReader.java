@@ -71,6 +71,12 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
    *  SortRecordReader (Sort.java:279-295) sets it when the inputs' dictionaries differ. */
   void setMergeMap(int[] map) { mergeMap = map; }
 
+  /** Utils.correctSAMRecordForMerging's PG / RG rewrite on the device (hbam_rewrite_groups) with
+   *  the table HipSortRecordReader builds from htsjdk's own merger. */
+  void setGroupTable(byte[] table) { groupTable = table; }
+  private byte[] groupTable;
+  private int groupStatus = Hbam.OK;
+
   SAMFileHeader header() { return codecHeader; }
   private SAMFileHeader codecHeader;
 
@@ -134,6 +140,15 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
           bad = b.get(ValueLayout.JAVA_LONG, 0);
         }
       }
+      if (groupTable != null && (mergeMap == null || bad < 0)) {
+        try (Arena a = Arena.ofConfined()) {
+          final MemorySegment t = a.allocateFrom(ValueLayout.JAVA_BYTE, groupTable);
+          final MemorySegment st = a.allocate(ValueLayout.JAVA_INT), er = a.allocate(ValueLayout.JAVA_LONG);
+          final int rc4 = (int) Hbam.REWRITE_GROUPS.invokeExact(hbam.context(), dev, t, (long) groupTable.length, st, er);
+          if (rc4 != Hbam.OK) throw new RuntimeIOException("hbam_rewrite_groups: " + hbam.lastError());
+          groupStatus = st.get(ValueLayout.JAVA_INT, 0);
+        }
+      }
       final int rc2 = (int) Hbam.COLUMNS_TO_HOST.invokeExact(hbam.context(), dev, host);
       if (rc2 != Hbam.OK) throw new RuntimeIOException("hbam_columns_to_host: " + hbam.lastError());
       hostLive = true;
@@ -144,6 +159,10 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     }
     n = host.get(ValueLayout.JAVA_LONG, Hbam.offsetOf("n_records"));
     status = host.get(ValueLayout.JAVA_INT, Hbam.offsetOf("status"));
+    if (groupStatus != Hbam.OK) {  // the rewrite stopped at record n (dv holds the records before it)
+      status = groupStatus;
+      groupStatus = Hbam.OK;
+    }
     if (status != Hbam.OK) last = true;
     if (mergeMap != null && bad >= 0 && bad < n) {
       // SAMRecord.setReferenceIndex against the record's own header throws here (:286-313)

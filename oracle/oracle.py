@@ -440,12 +440,231 @@ def correct_payloads(pay, off, keys, ref_map):
     return pay, keys, -1
 
 
+def bam_header_text(data):
+    """The SAM text of a BAM header (zlib over the first members)."""
+    import struct
+    import zlib
+    d = bytes(np.asarray(data, np.uint8)[:64 << 20])
+    u, p = b"", 0
+    while p + 18 <= len(d):
+        bs = struct.unpack_from("<H", d, p + 16)[0] + 1
+        u += zlib.decompressobj(-15).decompress(d[p + 18:p + bs - 8])
+        p += bs
+        if len(u) >= 8 and len(u) >= 8 + struct.unpack_from("<i", u, 4)[0]:
+            return u[8:8 + struct.unpack_from("<i", u, 4)[0]]
+    raise ValueError("truncated header")
+
+
+def _group_lines(text, tag):
+    recs = []
+    for ln in text.split(b"\n"):
+        if not ln.startswith(tag + b"\t"):
+            continue
+        fields = {}
+        order = []
+        for f in ln.split(b"\t")[1:]:
+            if len(f) < 3:
+                continue
+            if f[:2] not in fields:
+                order.append(f[:2])
+            fields[f[:2]] = f[3:]
+        recs.append((fields.get(b"ID", b""), fields, order))
+    return recs
+
+
+def _merge_records(pairs, taken, translation):
+    """SamFileHeaderMerger.mergeHeaderRecords (htsjdk 1.131; restated: parity unpinned)."""
+    groups = []  # [(id, [(attrs-without-ID, [input])])] in first-seen order
+    for inp, rid, fields in pairs:
+        attrs = {k: v for k, v in fields.items() if k != b"ID"}
+        g = next((x for x in groups if x[0] == rid), None)
+        if g is None:
+            g = (rid, [])
+            groups.append(g)
+        v = next((x for x in g[1] if x[0] == attrs), None)
+        if v is None:
+            v = (attrs, [])
+            g[1].append(v)
+        v[1].append(inp)
+    collision = False
+    merged = []
+    for rid, variants in groups:
+        for attrs, inputs in variants:
+            if rid in taken:
+                collision = True
+                i = 1
+                while (rid + b".%d" % i) in taken:
+                    i += 1
+                new = rid + b".%d" % i
+            else:
+                new = rid
+            taken.add(new)
+            for inp in inputs:
+                translation.setdefault(inp, {})[rid] = new
+            merged.append((new, attrs))
+    return collision, merged
+
+
+def header_groups(texts):
+    """mergeReadGroups / mergeProgramGroups over the inputs' header texts -> dict(rg_collisions,
+    pg_collisions, rg (per-input id translation), pg (per-input; absent = no @PG record))."""
+    for t in texts:
+        for tag in (b"@RG", b"@PG"):
+            ids = [r[0] for r in _group_lines(t, tag)]
+            if len(set(ids)) != len(ids):
+                raise ValueError("duplicate %s id in one input" % tag.decode())
+    rg_tr = {}
+    rg_col, _ = _merge_records([(i, rid, f) for i, t in enumerate(texts) for rid, f, _ in _group_lines(t, b"@RG")],
+                               set(), rg_tr)
+    pending = [(i, rid, dict(f)) for i, t in enumerate(texts) for rid, f, _ in _group_lines(t, b"@PG")]
+    current = [x for x in pending if b"PP" not in x[2]]
+    pending = [x for x in pending if b"PP" in x[2]]
+    taken, pg_tr, pg_col = set(), {}, False
+    while current:
+        c, _ = _merge_records(current, taken, pg_tr)
+        pg_col = pg_col or c
+        current = [(i, pg_tr.get(i, {}).get(rid, rid), f) for i, rid, f in current]
+        moved = []
+        for i, rid, f in pending:
+            f = dict(f)
+            t = pg_tr.get(i, {})
+            if f[b"PP"] in t:
+                f[b"PP"] = t[f[b"PP"]]
+            moved.append((i, rid, f))
+        pending = moved
+        current, pending = ([x for x in pending if any(x[0] == y[0] and x[2][b"PP"] == y[1] for y in current)],
+                            [x for x in pending if not any(x[0] == y[0] and x[2][b"PP"] == y[1] for y in current)])
+    if pending:
+        raise ValueError("program groups whose PP points nowhere")
+    return {"rg_collisions": rg_col, "pg_collisions": pg_col, "rg": rg_tr, "pg": pg_tr}
+
+
+class GroupRewriteError(Exception):
+    def __init__(self, kind, record):
+        super().__init__("%s at record %d" % (kind, record))
+        self.kind, self.record = kind, record
+
+
+def _aux_items(aux):
+    """[(tag, type, value bytes)] of a BAM aux block; raises ValueError if it does not parse."""
+    import struct
+    out, p = [], 0
+    sizes = {b"A": 1, b"c": 1, b"C": 1, b"s": 2, b"S": 2, b"i": 4, b"I": 4, b"f": 4}
+    while p < len(aux):
+        if len(aux) - p < 3:
+            raise ValueError("aux")
+        tag, ty = aux[p:p + 2], aux[p + 2:p + 3]
+        q = p + 3
+        if ty in sizes:
+            n = sizes[ty]
+        elif ty in (b"Z", b"H"):
+            z = aux.find(b"\0", q)
+            if z < 0:
+                raise ValueError("aux")
+            n = z - q + 1
+        elif ty == b"B":
+            if len(aux) - q < 5:
+                raise ValueError("aux")
+            st = aux[q:q + 1]
+            es = {b"c": 1, b"C": 1, b"s": 2, b"S": 2, b"i": 4, b"I": 4, b"f": 4}.get(st)
+            if es is None:
+                raise ValueError("aux")
+            n = 5 + es * struct.unpack_from("<I", aux, q + 1)[0]
+        else:
+            raise ValueError("aux")
+        if q + n > len(aux):
+            raise ValueError("aux")
+        out.append((tag, ty, aux[q:q + n]))
+        p = q + n
+    return out
+
+
+def _int_type(v):
+    """BinaryTagCodec.getIntegerType"""
+    if v > 2147483647:
+        return b"I"
+    if v > 65535:
+        return b"i"
+    if v > 255:
+        return b"S"
+    if v > 127:
+        return b"C"
+    if v >= -128:
+        return b"c"
+    if v >= -32768:
+        return b"s"
+    return b"i"
+
+
+def rewrite_group_tags(pay, off, groups, inp):
+    """Utils.correctSAMRecordForMerging's PG / RG rewrite (cli/Utils.java:314-324) of input `inp`'s
+    SAMRecordWritable payloads, and BAMRecordCodec.encode of every record on which setAttribute ran
+    (htsjdk 1.131 restated, parity unpinned: integers re-typed, pad nibble 0, absent qualities
+    0xFF, bin 0 when unplaced; a replaced tag keeps its place).  -> (payload, offsets); raises
+    GroupRewriteError(kind, record) where the reference's map task fails."""
+    import struct
+    pg_map = groups["pg"].get(inp)  # the RG lookup uses the PROGRAM-group table too (:322)
+    todo = [t for t, c in ((b"PG", groups["pg_collisions"]), (b"RG", groups["rg_collisions"])) if c]
+    out = []
+    for i in range(len(off) - 1):
+        r = bytes(pay[int(off[i]):int(off[i + 1])])
+        if not todo:
+            out.append(r)
+            continue
+        lrn, nc, ls = r[12], struct.unpack_from("<H", r, 16)[0], max(0, struct.unpack_from("<i", r, 20)[0])
+        head = 36 + lrn + 4 * nc
+        vstart = head + (ls + 1) // 2 + ls
+        try:
+            items = _aux_items(r[vstart:])
+        except ValueError:
+            raise GroupRewriteError("SAMFormatException", i)
+        edits = {}
+        for t in todo:
+            first = next((k for k, it in enumerate(items) if it[0] == t), None)
+            if first is None:
+                continue
+            if items[first][1] != b"Z":
+                raise GroupRewriteError("ClassCastException", i)
+            if pg_map is None:
+                raise GroupRewriteError("NullPointerException", i)
+            edits[first] = pg_map.get(items[first][2][:-1])
+        if not edits:
+            out.append(r)
+            continue
+        aux = b""
+        for k, (tag, ty, val) in enumerate(items):
+            if k in edits:
+                if edits[k] is not None:
+                    aux += tag + b"Z" + edits[k] + b"\0"
+            elif ty in (b"c", b"C", b"s", b"S", b"i", b"I"):
+                v = struct.unpack("<" + {b"c": "b", b"C": "B", b"s": "h", b"S": "H", b"i": "i", b"I": "I"}[ty], val)[0]
+                nt = _int_type(v)
+                aux += tag + nt + struct.pack("<" + {b"c": "b", b"C": "B", b"s": "h", b"S": "H", b"i": "i", b"I": "I"}[nt], v)
+            else:
+                aux += tag + ty + val
+        seq = bytearray(r[head:head + (ls + 1) // 2])
+        if ls & 1:
+            seq[-1] &= 0xF0
+        qual = r[head + (ls + 1) // 2:vstart]
+        if ls and qual[0] == 0xFF:
+            qual = b"\xff" * ls
+        fixed = bytearray(r[:head])
+        if struct.unpack_from("<i", r, 4)[0] < 0:
+            struct.pack_into("<H", fixed, 14, 0)
+        body = bytes(fixed[4:]) + bytes(seq) + qual + aux
+        out.append(struct.pack("<i", len(body)) + body)
+    offs = np.zeros(len(out) + 1, np.int64)
+    offs[1:] = np.cumsum([len(x) for x in out])
+    return np.frombuffer(b"".join(out), np.uint8), offs
+
+
 def sort_merged(datas):
     """The multi-input Sort's total order over whole-file reads of every input: (key, input
     index, voffset) -> (keys, payload, offsets, merged dictionary)."""
     dicts = [bam_dictionary(d) for d in datas]
     merged, did = merged_dictionary(dicts)
     names = [n for n, _ in merged]
+    groups = header_groups([bam_header_text(d) for d in datas])
     K, P, O, F, V = [], [], [], [], []
     for fi, (d, dic) in enumerate(zip(datas, dicts)):
         h = read_header(d)
@@ -456,6 +675,7 @@ def sort_merged(datas):
             pay, keys, bad = correct_payloads(pay, off, keys, [names.index(n) for n, _ in dic])
             if bad >= 0:
                 raise ValueError("input %d record %d: index outside its dictionary" % (fi, bad))
+        pay, off = rewrite_group_tags(pay, off, groups, fi)
         for i in range(cols["n"]):
             P.append(bytes(pay[int(off[i]):int(off[i + 1])]))
         K.append(keys)

@@ -124,3 +124,45 @@ def redictionary_bam(data, prepend=((b"chrNEW", 5000),), drop_last=1):
             struct.pack_into("<i", r, 24, mref + k)
         out.append(bytes(r))
     return np.frombuffer(bgzf_pack(b"".join(out)), np.uint8).copy(), refs, new_refs
+
+
+def regroup_bam(data, text_fn, rg_fn):
+    """A copy of a BAM with its header text replaced by text_fn(text) and each record's first RG
+    tag replaced by rg_fn(i, value): None drops the tag, bytes = a new Z value, (type, raw) any
+    typed value (multi-input Sort group-collision tests)."""
+    import struct
+    import oracle
+    u = bam_stream(data)
+    lt = struct.unpack_from("<i", u, 4)[0]
+    text = text_fn(u[8:8 + lt])
+    p = 8 + lt
+    n = struct.unpack_from("<i", u, p)[0]
+    q = p + 4
+    for _ in range(n):
+        q += 8 + struct.unpack_from("<i", u, q)[0]
+    out = [b"BAM\x01", struct.pack("<i", len(text)), text, u[p:q]]
+    i = 0
+    while q + 4 <= len(u):
+        bs = struct.unpack_from("<i", u, q)[0]
+        r = u[q:q + 4 + bs]
+        q += 4 + bs
+        lrn, nc, ls = r[12], struct.unpack_from("<H", r, 16)[0], max(0, struct.unpack_from("<i", r, 20)[0])
+        vstart = 36 + lrn + 4 * nc + (ls + 1) // 2 + ls
+        items = oracle._aux_items(r[vstart:])
+        aux, done = b"", False
+        for tag, ty, val in items:
+            if tag == b"RG" and not done:
+                done = True
+                new = rg_fn(i, val[:-1] if ty == b"Z" else val)
+                if new is None:
+                    continue
+                if isinstance(new, tuple):
+                    aux += tag + new[0] + new[1]
+                else:
+                    aux += tag + b"Z" + new + b"\0"
+            else:
+                aux += tag + ty + val
+        body = r[4:vstart] + aux
+        out.append(struct.pack("<i", len(body)) + body)
+        i += 1
+    return np.frombuffer(bgzf_pack(b"".join(out)), np.uint8).copy()

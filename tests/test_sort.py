@@ -362,18 +362,47 @@ def test_header_merger_matches_oracle_restatement():
         oracle.merged_dictionary(bad)
 
 
-def test_header_merger_group_collisions_unsupported():
-    sys.path.insert(0, os.path.join(ROOT, "hadoop-bam_amd"))
+_GROUP_HEADERS = [
+    # identical groups: nothing renamed
+    [b"@RG\tID:g1\tSM:s1\n@PG\tID:p\tPN:x\n", b"@RG\tID:g1\tSM:s1\n@PG\tID:p\tPN:x\n"],
+    # RG and PG collisions, a PP chain whose root is renamed (so its child differs too)
+    [b"@RG\tID:g1\tSM:s1\n@PG\tID:bwa\tPN:bwa\n@PG\tID:gatk\tPN:gatk\tPP:bwa\n",
+     b"@RG\tID:g1\tSM:other\n@RG\tID:g2\tSM:s2\n@PG\tID:bwa\tPN:bwa\tVN:2\n@PG\tID:gatk\tPN:gatk\tPP:bwa\n"],
+    # three inputs, a taken suffix (g1.1 exists already), an input without @PG
+    [b"@RG\tID:g1\tSM:a\n@RG\tID:g1.1\tSM:z\n@PG\tID:p\tPN:x\n", b"@RG\tID:g1\tSM:b\n",
+     b"@RG\tID:g1\tSM:c\n@PG\tID:p\tPN:y\n@PG\tID:q\tPN:q\tPP:p\n@PG\tID:r\tPN:r\tPP:q\n"],
+    # a chain in one input only, PG ids shared by unrelated records
+    [b"@PG\tID:a\tPN:1\n@PG\tID:b\tPN:2\tPP:a\n", b"@PG\tID:b\tPN:2\n@PG\tID:a\tPN:3\tPP:b\n"],
+]
+
+
+@pytest.mark.parametrize("case", range(len(_GROUP_HEADERS)))
+def test_header_merger_groups_match_oracle(case):
+    """SamFileHeaderMerger's read-/program-group merge (mergeReadGroups / mergeProgramGroups:
+    collisions renamed ID.1, ID.2 ..., PP chains merged root first) against the oracle's
+    independent restatement (both parity unpinned: htsjdk 1.131 is absent)."""
+    sys.path[:0] = [os.path.join(ROOT, "hadoop-bam_amd"), os.path.join(ROOT, "oracle")]
+    import oracle
     from hadoop_bam.output import SAMFileHeader
     from hadoop_bam.sort import SamFileHeaderMerger
-    a = _dicts()
-    h1 = SAMFileHeader(b"@RG\tID:g1\tSM:s1\n", a)
-    h2 = SAMFileHeader(b"@RG\tID:g1\tSM:s1\n", a)
-    h3 = SAMFileHeader(b"@RG\tID:g1\tSM:other\n", a)
-    m = SamFileHeaderMerger("coordinate", [h1, h2])  # identical records: one merged record
-    assert m.getMergedHeader().text.count(b"@RG") == 1
-    with pytest.raises(NotImplementedError):
-        SamFileHeaderMerger("coordinate", [h1, h3])
+    texts = _GROUP_HEADERS[case]
+    m = SamFileHeaderMerger("coordinate", [SAMFileHeader(t, _dicts()) for t in texts])
+    want = oracle.header_groups(texts)
+    assert m.has_read_group_collisions == want["rg_collisions"]
+    assert m.has_program_group_collisions == want["pg_collisions"]
+    assert m.rg_tables == want["rg"] and m.pg_tables == want["pg"]
+    mh = m.getMergedHeader().text
+    for i, t in enumerate(texts):  # every input's renamed ids are in the merged header
+        for rid, new in list(m.rg_tables.get(i, {}).items()) + list(m.pg_tables.get(i, {}).items()):
+            assert (b"\tID:" + new + b"\t") in mh or mh.count(b"ID:" + new + b"\n")
+    if case == 1:
+        assert m.pg_tables[1] == {b"bwa": b"bwa.1", b"gatk": b"gatk.1"}
+        assert b"@PG\tID:gatk.1\tPN:gatk\tPP:bwa.1" in mh
+    if case == 2:
+        # ids are taken in processing order (idsThatAreAlreadyTaken grows as records merge), so
+        # input 1 gets g1.1 and input 0's own g1.1 record, processed after, becomes g1.1.1
+        assert m.rg_tables[1] == {b"g1": b"g1.1"} and m.rg_tables[0][b"g1.1"] == b"g1.1.1"
+        assert 1 not in m.pg_tables
 
 
 @pytest.mark.gpu
@@ -433,4 +462,66 @@ def test_multi_input_sort_index_outside_input_dictionary():
     with pytest.raises(ValueError):
         oracle.sort_merged([a, b])
     with pytest.raises(ValueError, match="input 0"):
+        sort_inputs(_lib.Context(0), [a, b])
+
+
+def _group_inputs(kind):
+    """small_pe.bam and a second input whose @RG / @PG records collide with it (kind: "mixed" —
+    RG values rewritten to a PG id, to an unknown id, dropped; "no_pg" — no @PG line in the second
+    header; "non_string" — one record's RG typed 'A')."""
+    sys.path[:0] = [os.path.join(ROOT, "hadoop-bam_amd"), os.path.join(ROOT, "oracle")]
+    from helpers import regroup_bam
+    a = np.fromfile(os.path.join(GOLDEN, "small_pe.bam"), dtype=np.uint8)
+
+    def text(t):
+        t = t.replace(b"SM:sample1", b"SM:sampleB").replace(b"PN:gen_bam\tVN:1", b"PN:gen_bam\tVN:2")
+        if kind == "no_pg":
+            t = b"".join(ln + b"\n" for ln in t.split(b"\n") if ln and not ln.startswith(b"@PG"))
+        return t
+
+    def rg(i, v):
+        if kind == "mixed":
+            return b"gen_bam" if i % 3 == 1 else b"zzz" if i % 5 == 2 else None if i % 7 == 3 else v
+        if kind == "non_string" and i == 11:
+            return (b"A", b"x")
+        return v
+    return a, regroup_bam(a, text, rg)
+
+
+@pytest.mark.gpu
+def test_multi_input_sort_group_collisions_match_oracle():
+    """Colliding @RG and @PG records: every record carrying RG / PG is rewritten through the
+    program-group table (cli/Utils.java:314-324; RG values that are not PG ids are removed, an RG
+    value naming a PG id takes its merged id) and re-encoded, on the device (hbam_rewrite_groups);
+    the sorted output equals the oracle's records byte for byte."""
+    import oracle
+    from hadoop_bam import _lib
+    from hadoop_bam.sort import sort_inputs
+    a, b = _group_inputs("mixed")
+    header, run = sort_inputs(_lib.Context(0), [a, b])
+    keys, pay, off, merged = oracle.sort_merged([a, b])
+    assert b"@RG\tID:grp1.1\tSM:sampleB" in header.text and b"@PG\tID:gen_bam.1" in header.text
+    assert run.n == len(keys)
+    assert np.array_equal(run.keys.cpu().numpy(), keys)
+    assert np.array_equal(run.offsets.cpu().numpy(), off)
+    assert np.array_equal(run.payload.cpu().numpy()[:len(pay)], pay)
+    # the quirk is visible: input 1's RG:gen_bam records now carry RG:gen_bam.1, and no record
+    # carries RG:grp1 (not a program-group id: removed)
+    assert pay.tobytes().count(b"RGZgen_bam.1\0") > 1000 and pay.tobytes().count(b"RGZgrp1\0") == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,exc", [("no_pg", "NullPointerException"), ("non_string", "ClassCastException")])
+def test_multi_input_sort_group_rewrite_exceptions(kind, exc):
+    """Where the reference's map task throws: an input without a program-group table meets a
+    record carrying RG (NullPointerException), an RG that is not a string (ClassCastException);
+    the oracle raises at the same record."""
+    import oracle
+    from hadoop_bam import _lib, formats
+    from hadoop_bam.sort import sort_inputs
+    a, b = _group_inputs(kind)
+    with pytest.raises(oracle.GroupRewriteError) as ei:
+        oracle.sort_merged([a, b])
+    assert ei.value.kind == exc
+    with pytest.raises(getattr(formats, exc), match="record %d of input 1" % ei.value.record):
         sort_inputs(_lib.Context(0), [a, b])

@@ -13,6 +13,7 @@
 #   sort,SIZE            tools/bench_sort.py (config #5 share)
 #   guess,SIZE           tools/bench_guess.py (config #3)
 #   crc                  tools/check_inflate_crc.py
+#   calib                rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/pmc_calib (known bytes per shape)
 #   py,SCRIPT[,ARGS..]   any repo script (ARGS separated by ',')
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -44,6 +45,10 @@ for spec in "$@"; do
       timeout -k 10 600 python -u tools/bench_sort.py --size ${a1:-12.5e9} > $O/sort.json 2> $O/sort.err; r=$? ;;
     guess)
       timeout -k 10 700 python -u tools/bench_guess.py --size ${a1:-50e9} --guesses 10000 --check 10000 > $O/guess.json 2> $O/guess.err; r=$? ;;
+    calib)  # FETCH_SIZE / WRITE_SIZE per access shape (tools/pmc_calib.hip, tools/pmc_calib.py)
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/calib_fetch -o run --output-format csv -- ./tools/pmc_calib > $O/calib.txt 2>&1 &&
+      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/calib_write -o run --output-format csv -- ./tools/pmc_calib > $O/calib_w.txt 2>&1; r=$?
+      [ $r -eq 0 ] && python3 tools/pmc_calib.py $O/calib.txt $(ls $O/calib_fetch/*counter_collection.csv $O/calib_fetch/*/*counter_collection.csv 2>/dev/null | head -1) $(ls $O/calib_write/*counter_collection.csv $O/calib_write/*/*counter_collection.csv 2>/dev/null | head -1) $O/calib.json > $O/calib_summary.txt 2>&1 ;;
     crc)
       timeout -k 10 900 python -u tools/check_inflate_crc.py > $O/crc.txt 2>&1; r=$? ;;
     py)
