@@ -296,17 +296,23 @@ __device__ int32_t bp_peek(BcfPbs& p, int32_t* c) {
   }
 }
 // the trailing cursor's next k bytes (k <= what the lead delivered); empty blocks read as
-// short reads there too
-__device__ void bp_take(BcfPbs& p, uint8_t* dst, int32_t k) {
+// short reads there too (-1, bounded by the blocks a window holds).  The lead already read these
+// bytes, so an error or a cursor that stops advancing "cannot happen": it ends the decode with
+// TribbleException instead of spinning.
+__device__ int32_t bp_take(BcfPbs& p, uint8_t* dst, int32_t k) {
+  int32_t stalls = 0;
   while (k > 0) {
-    int32_t got;
-    if (bc_read(p.tr, dst, k, &got) || got <= 0) {  // cannot happen: the lead read these bytes
-      if (got == 0) return;
+    int32_t got = 0;
+    const int32_t rc = bc_read(p.tr, dst, k, &got);
+    if (rc) return HBAM_ETRIBBLE;
+    if (got <= 0) {
+      if (got == 0 || ++stalls > 16384) return HBAM_ETRIBBLE;
       continue;
     }
     if (dst) dst += got;
     k -= got;
   }
+  return HBAM_OK;
 }
 // read(bytes, 0, len): *got = bytes or -1
 __device__ int32_t bp_read(BcfPbs& p, uint8_t* dst, int32_t len, int32_t* got) {
@@ -323,7 +329,7 @@ __device__ int32_t bp_read(BcfPbs& p, uint8_t* dst, int32_t len, int32_t* got) {
     }
     int32_t k = p.n_chars - p.next;
     if (k > len - n) k = len - n;
-    bp_take(p, dst ? dst + n : nullptr, k);
+    if ((rc = bp_take(p, dst ? dst + n : nullptr, k))) return rc;
     p.next += k;
     n += k;
   }
@@ -373,8 +379,8 @@ __device__ int32_t bcf_decode_pbs(BcfPbs& p, const BcfHdr& h, uint8_t* site_scra
     if (rc) return rc;
     uint32_t byte = 0xffu;
     if (c >= 0) {
-      uint8_t t;
-      bp_take(p, &t, 1);
+      uint8_t t = 0;
+      if ((rc = bp_take(p, &t, 1))) return rc;
       byte = t;
       ++p.next;
       ++p.position;

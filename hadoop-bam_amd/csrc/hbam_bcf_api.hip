@@ -283,8 +283,10 @@ extern "C" int hbam_bcf_decode_split(hbam_ctx* c, const uint8_t* comp, int on_de
   if (!c || !comp || !h || !out) return HBAM_EINVAL;
   memset(out, 0, sizeof *out);
   HIPCHK(c, hipSetDevice(c->device));
-  if (comp_base + comp_len != file_len)
-    return set_err(c, HBAM_EINVAL, "a BCF split reads to the end of the file: the window must reach it");
+  if (comp_base + comp_len > file_len) return set_err(c, HBAM_EINVAL, "window past the end of the file");
+  const bool window_is_file_end = comp_base + comp_len == file_len;
+  if (!h->bgzf && !window_is_file_end)
+    return set_err(c, HBAM_EINVAL, "an uncompressed BCF split reads to the end of the file: the window must reach it");
   c->timing = hbam_timing{};
   const uint8_t* d;
   int rc = stage_comp(c, comp, on_device, comp_len, &d);
@@ -304,9 +306,13 @@ extern "C" int hbam_bcf_decode_split(hbam_ctx* c, const uint8_t* comp, int on_de
     if (coff_s < comp_base || coff_s > comp_base + comp_len)
       return set_err(c, HBAM_EINVAL, "v_start outside the compressed window");
     Chain ch;
-    if ((rc = build_chain(c, d, comp_len, coff_s - comp_base, true, &ch))) return rc;
+    if ((rc = build_chain(c, d, comp_len, coff_s - comp_base, window_is_file_end, &ch))) return rc;
     const uint64_t nb = ch.nb;
     if (nb == 0) {  // initialize(): bci.seek(virtualStart) fails, or an empty stream
+      if (ch.end_code == HBAM_EMORE) {
+        out->status = HBAM_EMORE;
+        return HBAM_OK;
+      }
       if (ch.end_code == HBAM_EEOF) {
         out->status = uoff_s != 0 ? HBAM_EIO : HBAM_OK;
         return HBAM_OK;
@@ -325,39 +331,65 @@ extern "C" int hbam_bcf_decode_split(hbam_ctx* c, const uint8_t* comp, int on_de
     k_isize32<<<grid_for(nb, 256), 256, 0, c->stream>>>(blk, nb, isz, (uint32_t*)small);
     uint64_t utotal = 0;
     if ((rc = scan_exclusive<uint32_t>(c, isz, nb, uoff, &utotal))) return rc;
-    uint8_t* ubw;
-    int32_t* st;
-    uint32_t* crc;
-    if ((rc = ensure(c, B_UBUF, utotal + UBUF_SLACK, &ubw)) || (rc = ensure(c, B_INFST, nb + 1, &st)) ||
-        (rc = ensure(c, B_CRC, nb + 1, &crc)))
-      return rc;
-    if ((rc = inflate_blocks(c, d, blk, nb, uoff, ubw, st, false, crc))) return rc;
-    unsigned long long* first_bad = (unsigned long long*)small + 1;
-    k_first_bad_block<<<grid_for(nb, 256), 256, 0, c->stream>>>(st, crc, blk, nb, 0, first_bad);
-    HIPCHK(c, hipGetLastError());
     std::vector<BlockRec> hb(nb);
     std::vector<uint64_t> hu(nb + 1);
     HIPCHK(c, hipMemcpyAsync(hb.data(), blk, nb * sizeof(BlockRec), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(hu.data(), uoff, (nb + 1) * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->pinned_small, small, 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    uint64_t fb = c->pinned_small[1];
     const uint32_t bigi = (uint32_t)(c->pinned_small[0] & 0xffffffffu);
+    // bci.seek(virtualStart): the block at coff_s, or the next one when it is empty
+    const uint64_t sblk = hb[0].isize == 0 ? 1 : 0;
+    // Where BGZFLimitingStream stops (the replay needs block sizes only): with every block assumed
+    // to inflate, the stream ends at z0; only the blocks up to z0's (and one more) are inflated, so
+    // a split costs its own blocks, not the rest of the file.  A block failing before
+    // that point ends the stream earlier: the replay runs again with it (z only moves back).
+    uint64_t z0 = 0;
+    int32_t zc0 = HBAM_OK;
+    if (sblk < nb) {
+      r0 = hu[sblk] + uoff_s;
+      const BcfBlocks B0{&hb, comp_base, nb, nb, HBAM_OK, ch.end_code};
+      if ((rc = bcf_stream_end(B0, sblk, uoff_s, r0, v_end, &z0, &zc0)))
+        return set_err(c, rc, "BGZFLimitingStream with vEnd & 0xffff == 0 never returns");
+      if (zc0 == HBAM_EMORE) {  // the stream runs past the window: the caller passes a longer one
+        out->status = HBAM_EMORE;
+        return HBAM_OK;
+      }
+    }
+    uint64_t nbi = nb;  // blocks inflated
+    if (sblk < nb) {
+      uint64_t zb = sblk;
+      while (zb + 1 < nb && hu[zb + 1] <= z0) ++zb;
+      nbi = std::min<uint64_t>(nb, zb + 2);
+    } else {
+      nbi = std::min<uint64_t>(nb, 2);
+    }
+    const uint64_t ui = hu[nbi];
+    uint8_t* ubw;
+    int32_t* st;
+    uint32_t* crc;
+    if ((rc = ensure(c, B_UBUF, ui + UBUF_SLACK, &ubw)) || (rc = ensure(c, B_INFST, nbi + 1, &st)) ||
+        (rc = ensure(c, B_CRC, nbi + 1, &crc)))
+      return rc;
+    if ((rc = inflate_blocks(c, d, blk, nbi, uoff, ubw, st, false, crc))) return rc;
+    unsigned long long* first_bad = (unsigned long long*)small + 1;
+    k_first_bad_block<<<grid_for(nbi, 256), 256, 0, c->stream>>>(st, crc, blk, nbi, 0, first_bad);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->pinned_small, small, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint64_t fb = c->pinned_small[1];
     int32_t fb_code = HBAM_EEOF;
     if (fb != ~0ULL) {
       int32_t s;
       HIPCHK(c, copy_sync(c, &s, st + fb, 4, hipMemcpyDeviceToHost));
       fb_code = (s == INF_DATA) ? HBAM_EDATA : HBAM_EFORMAT;
     }
-    if (bigi != 0xffffffffu && (fb == ~0ULL || bigi < fb)) {
+    if (bigi != 0xffffffffu && bigi < nbi && (fb == ~0ULL || bigi < fb)) {
       fb = bigi;
       fb_code = HBAM_EUNSUPPORTED;
     }
     if (fb == ~0ULL) fb = nb;
-    // bci.seek(virtualStart): the block at coff_s, or the next one when it is empty
-    uint64_t sblk = 0;
     if (fb == 0) { out->status = fb_code; return HBAM_OK; }
-    if (hb[0].isize == 0) sblk = 1;
     if (sblk >= nb) {
       if (ch.end_code != HBAM_EEOF) { out->status = ch.end_code == HBAM_ERUNTIMEIO ? HBAM_EIO : ch.end_code; return HBAM_OK; }
       out->status = uoff_s != 0 ? HBAM_EIO : HBAM_OK;
@@ -370,14 +402,17 @@ extern "C" int hbam_bcf_decode_split(hbam_ctx* c, const uint8_t* comp, int on_de
       const bool eof = (after == file_len) || (file_len - after == 28);
       if (uoff_s > bs.isize || (uoff_s == bs.isize && !eof)) { out->status = HBAM_EIO; return HBAM_OK; }
     }
-    r0 = hu[sblk] + uoff_s;
-    const BcfBlocks B{&hb, comp_base, nb, fb, fb_code, ch.end_code};
-    if ((rc = bcf_stream_end(B, sblk, uoff_s, r0, v_end, &z, &z_code)))
-      return set_err(c, rc, "BGZFLimitingStream with vEnd & 0xffff == 0 never returns");
+    z = z0;
+    z_code = zc0;
+    if (fb < nb) {
+      const BcfBlocks B{&hb, comp_base, nb, fb, fb_code, ch.end_code};
+      if ((rc = bcf_stream_end(B, sblk, uoff_s, r0, v_end, &z, &z_code)))
+        return set_err(c, rc, "BGZFLimitingStream with vEnd & 0xffff == 0 never returns");
+    }
     ub = ubw;
-    ulen = utotal;
+    ulen = ui;
     uo = uoff + sblk;
-    wb = nb - sblk;
+    wb = nbi - sblk;
     rel_base = r0;
   } else {
     // FileSplit: the header is read through the stream first, then skip(start - position)

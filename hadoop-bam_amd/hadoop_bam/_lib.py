@@ -331,8 +331,17 @@ class Context:
                 if not data.is_contiguous():
                     raise ValueError("device input must be contiguous")
                 import torch
+                nbytes = data.numel() * data.element_size()
+                # the kernels read whole 16-byte quads and fixed windows past the last byte: 64
+                # readable bytes must follow (include/hbam.h); a view that ends at (or near) the end
+                # of its allocation is copied into a padded buffer first
+                room = data.untyped_storage().nbytes() - data.storage_offset() * data.element_size()
+                if room < nbytes + 64:
+                    pad = torch.zeros(nbytes + 64, dtype=torch.uint8, device=data.device)
+                    pad[:nbytes].copy_(data.reshape(-1).view(torch.uint8))
+                    data = pad
                 torch.cuda.current_stream(data.device).synchronize()
-                return C.c_void_p(data.data_ptr()), data.numel() * data.element_size(), 1, data
+                return C.c_void_p(data.data_ptr()), nbytes, 1, data
             a = data.numpy()
         elif isinstance(data, np.ndarray):
             a = np.ascontiguousarray(data, dtype=np.uint8)

@@ -105,6 +105,9 @@ class BCFRecord:
         return bytes(self._c["data"][o:o + n])
 
 
+BCF_WINDOW_TAIL = 1 << 20  # compressed bytes read past vEnd's block offset at first
+
+
 class BCFRecordReader:
     """BCFRecordReader.java:52-175.  FileVirtualSplit (BGZF, read through BGZFLimitingStream
     :177-237) or FileSplit (uncompressed); key = contig index << 32 | (start - 1)."""
@@ -126,11 +129,21 @@ class BCFRecordReader:
         else:
             base = min(max(split.getStart(), h["header_len"]), ss.length)
             start, end = split.getStart(), split.getLength()
-        window = ss.read_at(base, ss.length - base)  # a BCF split reads to the end of the file
-        cols = ctx.bcf_decode_split(window, h, start, end, comp_base=base, file_len=ss.length,
-                                    keep_data=self.keep)
-        if cols["rc"]:
-            raise_for(cols["rc"], cols.get("error", ""))
+        # BGZF: the split's own bytes to past vEnd's block, longer only while BGZFLimitingStream
+        # runs past the window (HBAM_EMORE: it stops only in a block starting exactly at vEnd's
+        # offset, :206); uncompressed: to the end of the file (the reader's bound is a length)
+        tail = BCF_WINDOW_TAIL
+        while True:
+            stop = ss.length if not h["bgzf"] else min(ss.length, (end >> 16) + tail)
+            window = ss.read_at(base, stop - base)
+            cols = ctx.bcf_decode_split(window, h, start, end, comp_base=base, file_len=ss.length,
+                                        keep_data=self.keep)
+            if cols["rc"]:
+                raise_for(cols["rc"], cols.get("error", ""))
+            if cols["status"] != _lib.HBAM_EMORE or stop == ss.length:
+                break
+            tail *= 4
+        self.window_bytes = stop - base
         self.cols, self.i = cols, -1
         self.key = None
 

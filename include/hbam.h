@@ -470,7 +470,9 @@ int hbam_resolve_tokens(hbam_ctx* ctx, uint8_t* io, uint32_t isize, const uint32
 typedef struct hbam_bcf_header {
   int32_t n_contig;       /* ##contig lines (BCF2Codec contigNames; CHROM indexes them) */
   int32_t n_sample;       /* header.getNGenotypeSamples() */
-  int32_t n_dict;         /* string dictionary: PASS + FILTER/INFO/FORMAT IDs (BCF2Utils.makeDictionary) */
+  int32_t n_dict;         /* string dictionary: PASS + FILTER/INFO/FORMAT IDs, first occurrence
+                             (BCF2Utils.makeDictionary; whether htsjdk 1.131's shouldBeAddedToDictionary()
+                             also admits ##ALT / ##contig lines is unverified: parity unpinned) */
   int32_t bgzf;           /* BlockCompressedInputStream.isValidFile(file) */
   uint64_t header_len;    /* uncompressed bytes of magic, l_text and the header text */
   uint64_t first_voffset; /* position of the first record: virtual offset (BGZF) or file offset */

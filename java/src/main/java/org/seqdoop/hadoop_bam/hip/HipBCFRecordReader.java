@@ -1,7 +1,9 @@
 // Drop-in body of org.seqdoop.hadoop_bam.BCFRecordReader (BCFRecordReader.java:52-175) over the C
-// ABI.  initialize() maps the split's file from its start to the end of the file (a BCF split
-// reads through BGZFLimitingStream, :177-237, which only stops in a block starting exactly at the
-// split end) and hbam_bcf_decode_split decodes every record on the device; nextKeyValue hands out
+// ABI.  initialize() maps the split's bytes from its start to 1 MiB past vEnd's block (a BGZF split
+// reads through BGZFLimitingStream, :177-237, which stops in a block starting exactly at the split
+// end; while it runs past the window, HBAM_EMORE, the window grows 4x, up to the end of the file;
+// an uncompressed split reads to the end of the file) and hbam_bcf_decode_split decodes every
+// record on the device, inflating only the blocks the stream reaches; nextKeyValue hands out
 // the key (contig index << 32 | start - 1, :167-171) and raises, after the last record, the
 // exception the reference's BCF2Codec.decode raises there.  getCurrentValue() exposes the raw
 // BCF2 record bytes and the decoded site fields (a VariantContext is built by the caller's
@@ -45,9 +47,13 @@ public class HipBCFRecordReader extends RecordReader<LongWritable, HipBCFRecordR
     arena = Arena.ofConfined();
     try (FileChannel ch = FileChannel.open(path, StandardOpenOption.READ)) {
       final long fileLen = ch.size();
-      final MemorySegment head = ch.map(FileChannel.MapMode.READ_ONLY, 0, Math.min(fileLen, 1 << 20), arena);
       final MemorySegment h = arena.allocate(Hbam.BCF_HEADER);
-      int rc = (int) Hbam.BCF_PARSE_HEADER.invokeExact(hbam.context(), head, head.byteSize(), h);
+      int rc;
+      for (long want = 1 << 20; ; want *= 4) {  // a header longer than the prefix: HBAM_EMORE, read more
+        final MemorySegment head = ch.map(FileChannel.MapMode.READ_ONLY, 0, Math.min(fileLen, want), arena);
+        rc = (int) Hbam.BCF_PARSE_HEADER.invokeExact(hbam.context(), head, head.byteSize(), h);
+        if (rc != Hbam.EMORE || want >= fileLen) break;
+      }
       if (rc != Hbam.OK) throw new IOException("BCF2Codec.readHeader: " + hbam.lastError());
       final long start, end, base;
       if (virt) {
@@ -59,13 +65,18 @@ public class HipBCFRecordReader extends RecordReader<LongWritable, HipBCFRecordR
         end = ((FileSplit) spl).getLength();
         base = Math.min(Math.max(start, h.get(ValueLayout.JAVA_LONG, 16)), fileLen);
       }
-      final MemorySegment win = ch.map(FileChannel.MapMode.READ_ONLY, base, fileLen - base, arena);
+      final boolean bgzf = h.get(ValueLayout.JAVA_INT, 12) != 0;
       final MemorySegment cols = arena.allocate(Hbam.BCF_COLUMNS);
-      rc = (int) Hbam.BCF_DECODE_SPLIT.invokeExact(hbam.context(), win, 0, base, fileLen - base, fileLen, h,
-                                                   start, end, cols);
-      if (rc != Hbam.OK) throw new IOException("hbam_bcf_decode_split: " + hbam.lastError());
+      for (long tail = 1 << 20; ; tail *= 4) {
+        final long stop = !bgzf ? fileLen : Math.min(fileLen, (end >>> 16) + tail);
+        final MemorySegment win = ch.map(FileChannel.MapMode.READ_ONLY, base, stop - base, arena);
+        rc = (int) Hbam.BCF_DECODE_SPLIT.invokeExact(hbam.context(), win, 0, base, stop - base, fileLen, h,
+                                                     start, end, cols);
+        if (rc != Hbam.OK) throw new IOException("hbam_bcf_decode_split: " + hbam.lastError());
+        status = cols.get(ValueLayout.JAVA_INT, 8);
+        if (status != Hbam.EMORE || stop == fileLen) break;
+      }
       n = cols.get(ValueLayout.JAVA_LONG, 0);
-      status = cols.get(ValueLayout.JAVA_INT, 8);
       keys = down(hbam, cols, "key", 8);
       chrom = down(hbam, cols, "chrom", 4);
       pos = down(hbam, cols, "pos", 4);

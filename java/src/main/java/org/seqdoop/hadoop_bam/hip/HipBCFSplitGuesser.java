@@ -25,21 +25,36 @@ public class HipBCFSplitGuesser {
     inFile = ss;
     hbam = HipBAMRecordReader.context(null);
     header = Arena.ofAuto().allocate(Hbam.BCF_HEADER);
-    final byte[] head = headerStream.readNBytes(1 << 20);
+    byte[] head = headerStream.readNBytes(1 << 20);
     final byte[] magic = Hbam.readWindow(ss, 0, 18);
-    try (Arena a = Arena.ofConfined()) {
-      final MemorySegment h = a.allocate(Math.max(head.length, 1));
-      MemorySegment.copy(head, 0, h, ValueLayout.JAVA_BYTE, 0, head.length);
-      final int rc = (int) Hbam.BCF_PARSE_HEADER.invokeExact(hbam.context(), h, (long) head.length, header);
+    for (;;) {  // a header longer than the prefix (HBAM_EMORE, e.g. many samples): read 4x more
+      int rc;
+      try (Arena a = Arena.ofConfined()) {
+        final MemorySegment h = a.allocate(Math.max(head.length, 1));
+        MemorySegment.copy(head, 0, h, ValueLayout.JAVA_BYTE, 0, head.length);
+        rc = (int) Hbam.BCF_PARSE_HEADER.invokeExact(hbam.context(), h, (long) head.length, header);
+      } catch (RuntimeException e) {
+        throw e;
+      } catch (Throwable t) {
+        throw new IOException(t);
+      }
+      if (rc == Hbam.EMORE) {
+        final byte[] more = headerStream.readNBytes(3 * head.length);
+        if (more.length > 0) {
+          final byte[] grown = java.util.Arrays.copyOf(head, head.length + more.length);
+          System.arraycopy(more, 0, grown, head.length, more.length);
+          head = grown;
+          continue;
+        }
+      }
       if (rc != Hbam.OK) throw Hbam.exceptionFor(rc, "BCF2Codec.readHeader: " + hbam.lastError());
-    } catch (IOException | RuntimeException e) {
-      throw e;
-    } catch (Throwable t) {
-      throw new IOException(t);
+      break;
     }
-    // BlockCompressedInputStream.isValidFile on the data stream (:99-103)
+    // BlockCompressedInputStream.isValidFile on the data stream (:99-103): the 16 header bytes
+    // hbam_bcf_parse_header and the mirror check (ID1 ID2 CM FLG, XLEN = 6, 'B' 'C', SLEN = 2)
     bgzf = magic.length == 18 && (magic[0] & 0xff) == 0x1f && (magic[1] & 0xff) == 0x8b && magic[2] == 8
-        && magic[3] == 4 && magic[12] == 'B' && magic[13] == 'C';
+        && magic[3] == 4 && magic[10] == 6 && magic[11] == 0 && magic[12] == 'B' && magic[13] == 'C'
+        && magic[14] == 2 && magic[15] == 0;
     header.set(ValueLayout.JAVA_INT, 12, bgzf ? 1 : 0);
   }
 

@@ -154,6 +154,9 @@ static int pbs_read(pbs* p, uint8_t* out, int32_t len, int32_t* got) {
 /* ---- BCF2 record decode (restated subset, see the file header) -------------------------- */
 typedef struct bcf_rec {
   int32_t l_shared, l_indiv, chrom, pos, rlen, n_allele, n_info, n_fmt, n_sample;
+  uint32_t qual;     /* QUAL float bits */
+  int32_t nai, nfs;  /* n_allele << 16 | n_info, n_fmt << 24 | n_sample as read */
+  uint8_t* indiv;    /* the genotype block, when the caller asked for it (bcf_decode_keep) */
 } bcf_rec;
 
 typedef struct bcf_bytes { /* the decoder's ByteArrayInputStream over one block */
@@ -245,8 +248,10 @@ static int bcf_decode(pbs* p, const or_bcf_hdr_s* h, bcf_rec* r, uint8_t** scrat
   if (r->chrom < 0 || r->chrom >= h->n_contig) return OR_ERUNTIME; /* contigNames.get */
   r->pos = bb_int(&b, 4);
   r->rlen = bb_int(&b, 4);
-  (void)bb_int(&b, 4); /* QUAL */
+  r->qual = (uint32_t)bb_int(&b, 4); /* QUAL */
   const int32_t nai = bb_int(&b, 4), nfs = bb_int(&b, 4);
+  r->nai = nai;
+  r->nfs = nfs;
   r->n_allele = nai >> 16;
   r->n_info = nai & 0xffff;
   r->n_fmt = nfs >> 24;
@@ -271,11 +276,17 @@ static int bcf_decode(pbs* p, const or_bcf_hdr_s* h, bcf_rec* r, uint8_t** scrat
   }
   if (r->n_fmt < 0 || r->n_allele < 1) return OR_ETRIBBLE; /* SitesInfoForDecoding.isValid */
   if (sz[1] < 0) return OR_ETRIBBLE;
-  { /* genotype block: read and dropped (decoded lazily) */
+  { /* genotype block: read and dropped (decoded lazily); kept in r->indiv when asked */
     int32_t n = 0;
+    uint8_t* keep = NULL;
+    if (r->indiv) {
+      keep = (uint8_t*)realloc(r->indiv, (size_t)sz[1] + 1);
+      if (!keep) return OR_ENOMEM;
+      r->indiv = keep;
+    }
     while (n < sz[1]) {
       int32_t got;
-      rc = pbs_read(p, NULL, sz[1] - n, &got);
+      rc = pbs_read(p, keep ? keep + n : NULL, sz[1] - n, &got);
       if (rc) return rc;
       if (got < 0) return OR_ETRIBBLE;
       n += got;
@@ -468,6 +479,7 @@ static int64_t g_guess_bcf(guesser* g, int64_t beg, int64_t end, int is_bgzf, co
           if (rc) break;
           if (c == -1) break;
           bcf_rec r;
+          r.indiv = NULL;
           rc = bcf_decode(&pb, h, &r, &scratch, &scap);
           if (rc != 1) break;
           rc = OR_OK;
@@ -483,6 +495,7 @@ static int64_t g_guess_bcf(guesser* g, int64_t beg, int64_t end, int is_bgzf, co
           if (rc) break;
           if (c == -1) break;
           bcf_rec r;
+          r.indiv = NULL;
           rc = bcf_decode(&pb, h, &r, &scratch, &scap);
           if (rc != 1) break;
           rc = OR_OK;
@@ -537,10 +550,26 @@ int64_t or_guess_bcf_record_start(const uint8_t* f, uint64_t len, int64_t beg, i
  * has read ahead, so the position is reported in the PBS's own coordinate: bytes from the split
  * start), CHROM, POS, key = (long)chrom << 32 | (long)pos.  Returns the count; *status = the
  * exception nextKeyValue raised after them (0 = clean end). */
+/* or_read_bcf_split plus every column BCFRecordReader's records carry (l_shared, l_indiv, rlen,
+ * QUAL bits, n_allele_info, n_fmt_sample) and each record's bytes (l_shared, l_indiv, the site
+ * block, the genotype block) concatenated into bytes[0, bytes_cap) at boff[i] (boff: cap + 1). */
+int64_t or_read_bcf_split_ex(const uint8_t* f, uint64_t len, int is_bgzf, uint64_t v_start, uint64_t v_end,
+                             int32_t n_contig, int32_t n_sample, int32_t n_dict, uint64_t header_len,
+                             int64_t* rel, int32_t* chrom, int32_t* pos, int64_t* key, int32_t* l_shared,
+                             int32_t* l_indiv, int32_t* rlen, uint32_t* qual, int32_t* nai, int32_t* nfs,
+                             uint8_t* bytes, uint64_t bytes_cap, uint64_t* boff, uint64_t cap, int* status);
 int64_t or_read_bcf_split(const uint8_t* f, uint64_t len, int is_bgzf, uint64_t v_start, uint64_t v_end,
                           int32_t n_contig, int32_t n_sample, int32_t n_dict, uint64_t header_len,
                           int64_t* rel, int32_t* chrom, int32_t* pos, int64_t* key, uint64_t cap,
                           int* status) {
+  return or_read_bcf_split_ex(f, len, is_bgzf, v_start, v_end, n_contig, n_sample, n_dict, header_len, rel,
+                              chrom, pos, key, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 0, NULL, cap, status);
+}
+int64_t or_read_bcf_split_ex(const uint8_t* f, uint64_t len, int is_bgzf, uint64_t v_start, uint64_t v_end,
+                             int32_t n_contig, int32_t n_sample, int32_t n_dict, uint64_t header_len,
+                             int64_t* rel, int32_t* chrom, int32_t* pos, int64_t* key, int32_t* l_shared,
+                             int32_t* l_indiv, int32_t* rlen, uint32_t* qual, int32_t* nai, int32_t* nfs,
+                             uint8_t* bytes, uint64_t bytes_cap, uint64_t* boff, uint64_t cap, int* status) {
   *status = OR_OK;
   const or_bcf_hdr_s h = {n_contig, n_sample, n_dict};
   ostream os = {f, (int64_t)len, 0};
@@ -578,9 +607,12 @@ int64_t or_read_bcf_split(const uint8_t* f, uint64_t len, int is_bgzf, uint64_t 
   }
   {
     uint8_t* scratch = NULL;
+    uint8_t* indiv = NULL;
     int32_t scap = 0;
     int64_t n = 0;
+    uint64_t bo = 0;
     const int64_t base = pb.position;
+    if (boff) boff[0] = 0;
     for (;;) {
       int32_t c;
       if ((rc = pbs_peek(&pb, &c))) { *status = rc; break; }
@@ -588,17 +620,40 @@ int64_t or_read_bcf_split(const uint8_t* f, uint64_t len, int is_bgzf, uint64_t 
       if (!is_bgzf && pb.position >= limit) break;
       const int64_t at = pb.position;
       bcf_rec r;
+      r.indiv = NULL;
+      r.indiv = bytes ? (indiv ? indiv : (uint8_t*)malloc(1)) : NULL;
       rc = bcf_decode(&pb, &h, &r, &scratch, &scap);
+      if (bytes) indiv = r.indiv;
       if (rc != 1) { *status = rc; break; }
       if ((uint64_t)n < cap) {
         rel[n] = is_bgzf ? at - base : at;
         chrom[n] = r.chrom;
         pos[n] = r.pos;
         key[n] = (int64_t)((uint64_t)(int64_t)r.chrom << 32 | (uint64_t)(int64_t)r.pos);
+        if (l_shared) {
+          l_shared[n] = r.l_shared;
+          l_indiv[n] = r.l_indiv;
+          rlen[n] = r.rlen;
+          qual[n] = r.qual;
+          nai[n] = r.nai;
+          nfs[n] = r.nfs;
+        }
+        if (bytes) {
+          const uint64_t need = 8 + (uint64_t)r.l_shared + (uint64_t)r.l_indiv;
+          if (bo + need <= bytes_cap) {
+            memcpy(bytes + bo, &r.l_shared, 4);
+            memcpy(bytes + bo + 4, &r.l_indiv, 4);
+            memcpy(bytes + bo + 8, scratch, (size_t)r.l_shared);
+            memcpy(bytes + bo + 8 + r.l_shared, indiv, (size_t)r.l_indiv);
+          }
+          bo += need;
+          boff[n + 1] = bo;
+        }
       }
       ++n;
     }
     free(scratch);
+    free(indiv);
     pbs_free(&pb);
     bcis_free(bz);
     return n;

@@ -789,6 +789,33 @@ def guess_bcf_record_start(data, beg, end, h):
     return r, err.value
 
 
+def read_bcf_split_ex(data, start, end_or_len, h, cap=1 << 20):
+    """read_bcf_split with every record column (l_shared, l_indiv, rlen, qual, n_allele_info,
+    n_fmt_sample) and each record's bytes (l_shared, l_indiv, site block, genotype block)."""
+    a, p = _buf(data)
+    cols = dict(rel=np.zeros(cap, np.int64), chrom=np.zeros(cap, np.int32), pos=np.zeros(cap, np.int32),
+                key=np.zeros(cap, np.int64), l_shared=np.zeros(cap, np.int32), l_indiv=np.zeros(cap, np.int32),
+                rlen=np.zeros(cap, np.int32), qual=np.zeros(cap, np.uint32), n_allele_info=np.zeros(cap, np.int32),
+                n_fmt_sample=np.zeros(cap, np.int32))
+    bcap = 2 * len(a) + (1 << 22)
+    byts = np.zeros(bcap, np.uint8)
+    boff = np.zeros(cap + 1, np.uint64)
+    st = C.c_int(0)
+    f = lib().or_read_bcf_split_ex
+    f.restype = C.c_int64
+    n = int(f(p, C.c_uint64(len(a)), C.c_int(int(h["bgzf"])), C.c_uint64(start), C.c_uint64(end_or_len),
+              C.c_int32(h["n_contig"]), C.c_int32(h["n_sample"]), C.c_int32(h["n_dict"]),
+              C.c_uint64(h["header_len"]), *[C.c_void_p(cols[k].ctypes.data) for k in
+                                             ("rel", "chrom", "pos", "key", "l_shared", "l_indiv", "rlen", "qual",
+                                              "n_allele_info", "n_fmt_sample")],
+              C.c_void_p(byts.ctypes.data), C.c_uint64(bcap), C.c_void_p(boff.ctypes.data), C.c_uint64(cap),
+              C.byref(st)))
+    m = min(n, cap)
+    out = {k: v[:m].copy() for k, v in cols.items()}
+    out.update(n=n, status=st.value, bytes=byts[:int(boff[m])].tobytes(), boff=boff[:m + 1].copy())
+    return out
+
+
 def read_bcf_split(data, start, end_or_len, h, cap=1 << 22):
     """BCFRecordReader over one split: BGZF -> FileVirtualSplit [start, end_or_len) (virtual);
     uncompressed -> FileSplit start, length = end_or_len.  dict(n, status, rel, chrom, pos, key)."""
