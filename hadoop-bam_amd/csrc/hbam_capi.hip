@@ -344,9 +344,16 @@ int build_chain(hbam_ctx* c, const uint8_t* dcomp, uint64_t comp_len, uint64_t s
                                                                  blk, nbad);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->pinned_small, small, 16, hipMemcpyDeviceToHost, c->stream));
+  // the chain's ends in the same round trip (used when no chunk overflowed)
+  if (ncand) {
+    HIPCHK(c, hipMemcpyAsync(c->pinned_small + 8, cand, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->pinned_small + 10, blk + (ncand - 1), sizeof(BlockRec), hipMemcpyDeviceToHost,
+                             c->stream));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const uint32_t ovf = ((uint32_t*)c->pinned_small)[0];
   uint32_t bad = ((uint32_t*)c->pinned_small)[1];
+  bool ends_known = ovf == 0;
   if (ovf) {
     // more than SCAN_CAP candidates in some chunk (blocks of < 1 KiB compressed, or data full
     // of magic patterns): the exact two-pass scan writes the whole candidate list
@@ -369,12 +376,14 @@ int build_chain(hbam_ctx* c, const uint8_t* dcomp, uint64_t comp_len, uint64_t s
   uint64_t first = ~0ULL;
   BlockRec last{};
   if (ncand) {
-    HIPCHK(c, hipMemcpyAsync(c->pinned_small, cand, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->pinned_small + 2, blk + (ncand - 1), sizeof(BlockRec),
-                             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    first = c->pinned_small[0];
-    memcpy(&last, c->pinned_small + 2, sizeof last);
+    if (!ends_known) {
+      HIPCHK(c, hipMemcpyAsync(c->pinned_small + 8, cand, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->pinned_small + 10, blk + (ncand - 1), sizeof(BlockRec),
+                               hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    first = c->pinned_small[8];
+    memcpy(&last, c->pinned_small + 10, sizeof last);
   }
   uint8_t hdr[32];
   auto classify_end = [&](uint64_t pos) -> int32_t {
@@ -937,13 +946,15 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   HIPCHK(c, hipMemsetAsync(small, 0xff, 8 * 8, c->stream));
   HIPCHK(c, hipMemsetAsync(small + 8, 0, 8 * 8, c->stream));
   k_isize32<<<grid_for(nb, 256), 256, 0, c->stream>>>(blk, nb, isz, (uint32_t*)small);
-  uint64_t utotal = 0;
-  if ((rc = scan_exclusive<uint32_t>(c, isz, nb, uoff, &utotal))) return rc;
-  // first blocks (host view) for the seek semantics
+  if ((rc = scan_exclusive<uint32_t>(c, isz, nb, uoff, nullptr))) return rc;
+  // the inflated total and the first blocks (host view, for the seek semantics): one round trip
   BlockRec b0[2];
-  HIPCHK(c, copy_sync(c, b0, blk, std::min<uint64_t>(nb, 2) * sizeof(BlockRec), hipMemcpyDeviceToHost));
-  uint32_t big_first;
-  HIPCHK(c, copy_sync(c, &big_first, small, 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small + 64, uoff + nb, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small + 66, blk, std::min<uint64_t>(nb, 2) * sizeof(BlockRec),
+                           hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t utotal = c->pinned_small[64];
+  memcpy(b0, c->pinned_small + 66, std::min<uint64_t>(nb, 2) * sizeof(BlockRec));
   // inflate
   uint8_t* ub;
   int32_t* st;
@@ -972,7 +983,6 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
     fb = bigi;
     fb_code = HBAM_EUNSUPPORTED;
   }
-  (void)big_first;
   // hard end: first failing block, else the chain end
   uint64_t hard_end;
   int32_t hard_code;
@@ -1003,9 +1013,8 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
     const uint64_t after = comp_base + bs.coff + bs.clen;  // file position after the block
     const bool eof = (after == file_len) || (file_len - after == 28);
     if (uoff_s > bs.isize || (uoff_s == bs.isize && !eof)) { out->status = HBAM_EIO; return HBAM_OK; }
-    uint64_t u0;
-    HIPCHK(c, copy_sync(c, &u0, uoff + sblk, 8, hipMemcpyDeviceToHost));
-    r0 = u0 + uoff_s;
+    // uoff[sblk] is 0: sblk is 1 only when block 0 is empty (uoff[1] = ISIZE 0)
+    r0 = uoff_s;
   }
   // events: empty blocks after the seek block, at positions <= hard_end, in block order (so
   // sorted by position: k_decode_fixed binary-searches them; any number of them)
@@ -1016,14 +1025,12 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if ((rc = ensure(c, B_EVFLAG, nbs + 1, &evflag)) || (rc = ensure(c, B_EVPOS, nbs + 1, &evpos))) return rc;
   k_empty_flags<<<grid_for(nbs, 256), 256, 0, c->stream>>>(blk + sblk, nbs, evflag);
   HIPCHK(c, hipGetLastError());
-  uint64_t nev64 = 0;
-  if ((rc = scan_exclusive(c, evflag, nbs, evpos, &nev64))) return rc;
-  if ((rc = ensure(c, B_EVENTS, nev64 + 1, &evd))) return rc;
-  if (nev64)
-    k_empty_scatter<<<grid_for(nbs, 256), 256, 0, c->stream>>>(uoff + sblk, evflag, evpos, nbs, evd);
+  // their count is read back with the record walk's stitch count below (one round trip); the
+  // list is sized for every block
+  if ((rc = scan_exclusive(c, evflag, nbs, evpos, nullptr))) return rc;
+  if ((rc = ensure(c, B_EVENTS, nbs + 1, &evd))) return rc;
+  k_empty_scatter<<<grid_for(nbs, 256), 256, 0, c->stream>>>(uoff + sblk, evflag, evpos, nbs, evd);
   HIPCHK(c, hipGetLastError());
-  if (nev64 > 0xffffffffull) return set_err(c, HBAM_EUNSUPPORTED, "more than 2^32-1 empty BGZF blocks");
-  const uint32_t nev = (uint32_t)nev64;
   // events beyond the hard end cannot be reached; keep them (empty_at checks <= hard_end)
 
   // ---- K5: record starts (blocks [sblk, nb))
@@ -1052,9 +1059,13 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if (wb > 1)
     k_stitch_check<<<grid_for(wb - 1, 256), 256, 0, c->stream>>>(entry, exitp, (uint32_t)wb, nbad_d,
                                                                  badlist, (uint32_t)wb, mark);
-  uint32_t nbad = 0;
-  HIPCHK(c, hipMemcpyAsync(&nbad, nbad_d, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small + 80, nbad_d, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small + 81, evpos + nbs, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  uint32_t nbad = (uint32_t)c->pinned_small[80];
+  const uint64_t nev64 = c->pinned_small[81];
+  if (nev64 > 0xffffffffull) return set_err(c, HBAM_EUNSUPPORTED, "more than 2^32-1 empty BGZF blocks");
+  const uint32_t nev = (uint32_t)nev64;
   if (nbad) {  // runs of mismatched blocks repaired in parallel, then whatever is left, in order
     k_chain_fix_par<<<grid_for(nbad, 64), 64, 0, c->stream>>>(ub, uo, (uint32_t)wb, hard_end, BamFmt{n_ref},
                                                                entry, rel, count, exitp, badlist, nbad, mark);
@@ -1122,10 +1133,21 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   }
   // ---- pools
   uint64_t tot_name = 0, tot_cig = 0, tot_seq = 0, tot_aux = 0;
-  if ((rc = scan_exclusive<uint32_t>(c, dc.name_len, n_final, dc.name_off, &tot_name))) return rc;
-  if ((rc = scan_exclusive<uint32_t>(c, dc.cigar_n, n_final, dc.cigar_off, &tot_cig))) return rc;
-  if ((rc = scan_exclusive<uint32_t>(c, dc.seq_len, n_final, dc.seq_off, &tot_seq))) return rc;
-  if ((rc = scan_exclusive<uint32_t>(c, dc.aux_len, n_final, dc.aux_off, &tot_aux))) return rc;
+  // the four pool scans, their totals read back in one round trip
+  if ((rc = scan_exclusive<uint32_t>(c, dc.name_len, n_final, dc.name_off, nullptr))) return rc;
+  if ((rc = scan_exclusive<uint32_t>(c, dc.cigar_n, n_final, dc.cigar_off, nullptr))) return rc;
+  if ((rc = scan_exclusive<uint32_t>(c, dc.seq_len, n_final, dc.seq_off, nullptr))) return rc;
+  if ((rc = scan_exclusive<uint32_t>(c, dc.aux_len, n_final, dc.aux_off, nullptr))) return rc;
+  {
+    const uint64_t* offs[4] = {dc.name_off, dc.cigar_off, dc.seq_off, dc.aux_off};
+    for (int q = 0; q < 4; ++q)
+      HIPCHK(c, hipMemcpyAsync(c->pinned_small + 96 + q, offs[q] + n_final, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    tot_name = c->pinned_small[96];
+    tot_cig = c->pinned_small[97];
+    tot_seq = c->pinned_small[98];
+    tot_aux = c->pinned_small[99];
+  }
   if ((rc = ensure(c, B_C_NAMES, tot_name + 1, &dc.names))) return rc;
   if ((rc = ensure(c, B_C_CIGARS, tot_cig + 1, &dc.cigars))) return rc;
   if ((rc = ensure(c, B_C_SEQ, tot_seq + 1, &dc.seq))) return rc;

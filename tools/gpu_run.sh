@@ -7,7 +7,8 @@
 #   smoke                __graft_entry__.smoke()
 #   bench[,STEPS]        python bench.py (default --steps 20 --warmup 3)
 #   prof                 rocprofv3 --kernel-trace --stats of a short bench.py run
-#   pmc,COUNTERS         one rocprofv3 --pmc pass (COUNTERS separated by '+') of a short run
+#   pmc,COUNTERS[,SIZE[,LIB]]  one rocprofv3 --pmc pass (COUNTERS separated by '+') over a decode
+#   bin,PATH             run a probe executable (tools/probes/*)
 #   abdecode,SIZE,LIBS   tools/ab_decode.py A/B of library builds (LIBS separated by '+')
 #   stream,SIZE,WINDOW   tools/bench_stream.py (config #4 share)
 #   sort,SIZE            tools/bench_sort.py (config #5 share)
@@ -35,8 +36,10 @@ for spec in "$@"; do
       timeout -k 10 600 python -u bench.py --steps ${a1:-20} --warmup 3 > $O/bench.json 2> $O/bench.err; r=$? ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --parity-splits 0 > $O/bench_prof.json 2> $O/prof.err; r=$? ;;
-    pmc)
-      timeout -s KILL 300 rocprofv3 --pmc ${a1//+/ } -d $O/pmc_${a1//+/_} -o run -- python3 tools/ab_decode.py --size ${a2:-2e9} --reps 1 --libs libhbam.so > $O/pmc_${a1//+/_}.txt 2>&1; r=$? ;;
+    pmc)  # pmc,COUNTERS[,SIZE[,LIB]]: one counter pass over a decode (csv per dispatch)
+      timeout -s KILL 300 rocprofv3 --pmc ${a1//+/ } -d $O/pmc_${a1//+/_} -o run --output-format csv -- python3 tools/ab_decode.py --size ${a2:-2e9} --reps 1 --digest 0 --libs ${a3:-libhbam.so} > $O/pmc_${a1//+/_}.txt 2>&1; r=$? ;;
+    bin)  # bin,PATH: a probe executable of the repository
+      timeout -k 10 300 ./$a1 > $O/$(basename $a1).txt 2>&1; r=$? ;;
     abdecode)
       timeout -k 10 900 python -u tools/ab_decode.py --size ${a1:-5e9} --reps ${a3:-3} --libs ${a2//+/ } > $O/ab_${a2//+/_}.txt 2>&1; r=$? ;;
     stream)
