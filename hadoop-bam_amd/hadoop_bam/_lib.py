@@ -321,8 +321,9 @@ class Context:
         return {n: getattr(t, n) for n, _ in Timing._fields_}
 
     @staticmethod
-    def _ptr(data):
-        """(pointer, length, on_device, keepalive) for bytes / numpy / torch cuda tensor."""
+    def _ptr(data, output=False):
+        """(pointer, length, on_device, keepalive) for bytes / numpy / torch cuda tensor.  An
+        output buffer (the library writes into it) is never replaced by a padded copy."""
         if hasattr(data, "data_ptr") and hasattr(data, "is_cuda"):
             if data.is_cuda:
                 # libhbam reads the raw pointer on its own stream: the bytes must be one dense
@@ -336,7 +337,7 @@ class Context:
                 # readable bytes must follow (include/hbam.h); a view that ends at (or near) the end
                 # of its allocation is copied into a padded buffer first
                 room = data.untyped_storage().nbytes() - data.storage_offset() * data.element_size()
-                if room < nbytes + 64:
+                if room < nbytes + 64 and not output:
                     pad = torch.zeros(nbytes + 64, dtype=torch.uint8, device=data.device)
                     pad[:nbytes].copy_(data.reshape(-1).view(torch.uint8))
                     data = pad
@@ -359,7 +360,7 @@ class Context:
         p, n, dev, keep = self._ptr(data)
         bound = int(self.L.hbam_bgzf_bound(n, block_size))
         if out is not None:
-            q, cap, odev, okeep = self._ptr(out)
+            q, cap, odev, okeep = self._ptr(out, output=True)
             r = self.L.hbam_bgzf_compress(self.h, p, dev, n, block_size, q, odev, cap)
             if r < 0:
                 raise RuntimeError("hbam_bgzf_compress failed (%d): %s" % (r, self.last_error()))
