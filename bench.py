@@ -405,7 +405,7 @@ def main():
     achieved = alg / (inf_ms / 1e3) / 1e9
     traffic, traffic_src = None, None
     # the newest committed PMC pass of this kernel over the same workload (tools/pmc_summarize.py)
-    for rnd, tree in (("r03", "round3"), ("r02", "round2")):
+    for rnd, tree in (("r04", "round4"), ("r03", "round3"), ("r02", "round2")):
         pmc = os.path.join(ROOT, "profiles", rnd, "pmc_k_inflate_tokens.json")
         if traffic is None and os.path.exists(pmc):
             try:

@@ -1154,9 +1154,15 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if ((rc = ensure(c, B_C_QUAL, tot_seq + 1, &dc.qual))) return rc;
   if ((rc = ensure(c, B_C_AUX, tot_aux + 1, &dc.aux))) return rc;
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
+#ifdef HBAM_POOLS_LDS
+  if (n_final)
+    k_decode_pools_lds<<<(uint32_t)std::min<uint64_t>((n_final + 63) / 64, 6144), 64, 0, c->stream>>>(
+        ub, n_final, rec_off, dc);
+#else
   if (n_final)
     k_decode_pools<<<(uint32_t)std::min<uint64_t>(grid_for(n_final, 256), POOLS_MAX_WG), 256, 0, c->stream>>>(
         ub, n_final, rec_off, dc);
+#endif
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2105,7 +2111,9 @@ extern "C" int hbam_device_alloc(hbam_ctx* c, uint64_t bytes, void** dev_out) {
   if (!c || !dev_out) return HBAM_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));
   void* d = nullptr;
-  if (hipMalloc(&d, bytes ? bytes : 1) != hipSuccess) {
+  // + 64 readable bytes past the end: a buffer from here may be handed back as a device input,
+  // which the kernels read in whole 16-byte quads and 28-32-byte windows (include/hbam.h)
+  if (hipMalloc(&d, bytes + 64) != hipSuccess) {
     (void)hipGetLastError();
     return set_err(c, HBAM_ENOMEM, "hbam_device_alloc(%llu) failed", (unsigned long long)bytes);
   }

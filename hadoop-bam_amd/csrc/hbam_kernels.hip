@@ -339,6 +339,12 @@ __device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64
 // LDS per block also allows (VGPRs 75 -> 64, 2 spilled): k_resolve 47.4 -> 42.6 ms at 10 GB
 #define HBAM_RS_WAVES 8
 #endif
+#ifndef HBAM_RS_DSC_AL
+#define HBAM_RS_DSC_AL 0
+#endif
+#ifndef HBAM_RS_DEPMASK
+#define HBAM_RS_DEPMASK 0
+#endif
 __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* __restrict__ blk,
                                                 const uint64_t* __restrict__ uoff, uint32_t nblk,
                                                 uint8_t* __restrict__ ubuf,
@@ -443,7 +449,13 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
       bool pre = false, ord = false;
       if (j < total) {
         const uint32_t p = s_pos[j];
+#if HBAM_RS_DSC_AL
+        // two dword-aligned reads + v_alignbit: a byte-aligned ds_read_b32 replays (64 cycles of
+        // the CU's LDS pipe, tools/probes/lds_align_bench.hip)
+        const uint32_t dsc = lds_rd32u(s_buf, lbase + p);
+#else
         const uint32_t dsc = *(const uint32_t*)(s_buf + lbase + p);
+#endif
         const uint32_t len = (dsc & 0xffu) + 3u;
         const uint32_t dist = ((dsc >> 8) & 0xffffu) + 1u;
         const uint32_t e = p - dist + (len < dist ? len : dist);
@@ -501,6 +513,43 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
     // its external source [p - dist, p - dist + min(len, dist)) is pending.  Every round
     // copies all ready matches at once and clears their bits, so the rounds are the depth of
     // the stretch's match dependency graph (the earliest pending match is always ready).
+#if HBAM_RS_DEPMASK
+    if (nord && nord <= 64u) {
+      // At most one ordered match per lane (94 % of stretches): dependencies as match-index
+      // ranges instead of a pending-byte bitmap.  Destinations are disjoint and in index order,
+      // so the ordered matches writing into match k's external source [a, e) are the index range
+      // [lo, hi): lo = #{k': end(k') <= a}, hi = #{k': p(k') < e} (< k).  A round is then a
+      // compare against the wave-uniform done mask and the copies: no LDS state besides the bytes.
+      const bool mine = lane < nord;
+      const uint64_t rec = mine ? rs_unpack(s_rec[RS_MAXM - 1 - lane], s_pos) : 0ull;
+      const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
+                     dist = (uint32_t)(rec >> 32) & 0xffffu, e = (uint32_t)(rec >> 48);
+      const uint32_t a = p - dist;
+      const uint32_t vp = mine ? p : 0xffffffffu, ve = mine ? p + len : 0xffffffffu;
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (uint32_t step = 32; step; step >>= 1) {
+        if (__shfl(ve, lo + step - 1u) <= a) lo += step;
+        if (__shfl(vp, hi + step - 1u) < e) hi += step;
+      }
+      const uint64_t need = (hi > lo && mine) ? ((hi - lo == 64u ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo) : 0ull;
+      uint64_t done = ~__ballot(mine);
+      bool fin = !mine;
+      for (;;) {
+        const bool ready = !fin && (done & need) == need;
+        if (ready) rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
+        rs_lds_order();
+        fin = fin || ready;
+        const uint64_t rb = __ballot(ready);
+        done |= rb;
+        if (!__any(!fin)) break;
+        if (rb == 0ull) {  // validated descriptors always make progress: corrupt
+          if (lane == 0) status[b] = INF_DATA;
+          return;
+        }
+      }
+    } else
+#endif
     if (nord) {
       for (uint32_t w = lane; w < RS_PW; w += 64) s_pend[w] = 0u;
       rs_wave_sync();
@@ -1134,6 +1183,134 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
     }
   }
 }
+
+#ifdef HBAM_POOLS_LDS
+// A/B variant: the tile's record bytes staged in LDS first.  k_decode_pools waits for one
+// 16-byte load per lane per unit step (one load in flight per wave: latency-bound, 80 % of wave
+// time parked); here the wave first copies the tile's whole source span ([first record's variable
+// part, last record's end), 16-byte aligned) into LDS with every load of the span in flight at
+// once, then numbers the units as above and reads them from LDS (aligned dwords + v_alignbit),
+// so only the stores touch HBM in the unit loop.  A tile whose span exceeds the LDS budget takes
+// the global path of k_decode_pools.
+#ifndef HBAM_POOLS_LDS_BYTES
+#define HBAM_POOLS_LDS_BYTES 24576
+#endif
+constexpr uint32_t PL_BYTES = HBAM_POOLS_LDS_BYTES;
+static __device__ __forceinline__ uint32_t pl_w(const uint8_t* s, uint32_t a) { return *(const uint32_t*)(s + a); }
+// 16 bytes at any LDS index x (reads up to x + 20)
+static __device__ __forceinline__ u32x4_a1 pl_rd16(const uint8_t* s, uint32_t x) {
+  const uint32_t a = x & ~3u, sh = (x & 3u) * 8u;
+  const uint32_t w0 = pl_w(s, a), w1 = pl_w(s, a + 4), w2 = pl_w(s, a + 8), w3 = pl_w(s, a + 12), w4 = pl_w(s, a + 16);
+  u32x4_a1 o;
+  o[0] = __builtin_amdgcn_alignbit(w1, w0, sh);
+  o[1] = __builtin_amdgcn_alignbit(w2, w1, sh);
+  o[2] = __builtin_amdgcn_alignbit(w3, w2, sh);
+  o[3] = __builtin_amdgcn_alignbit(w4, w3, sh);
+  return o;
+}
+static __device__ __forceinline__ uint64_t pl_rd8(const uint8_t* s, uint32_t x) {
+  const uint32_t a = x & ~3u, sh = (x & 3u) * 8u;
+  const uint32_t w0 = pl_w(s, a), w1 = pl_w(s, a + 4), w2 = pl_w(s, a + 8);
+  return (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) | (uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32;
+}
+static __device__ __forceinline__ u32x4_a1 seq16_q(uint64_t q) {
+  u32x4_a1 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = seq4((uint32_t)(q >> (16 * j)) & 0xffu, (uint32_t)(q >> (16 * j + 8)) & 0xffu);
+  return o;
+}
+__global__ __launch_bounds__(64) void k_decode_pools_lds(const uint8_t* __restrict__ u, uint64_t nrec,
+                                                         const uint64_t* __restrict__ rec_off,
+                                                         DevColumns c) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_src[PL_BYTES + 32];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t ntiles = (nrec + 63) / 64;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint64_t r = t * 64 + lane;
+    const uint64_t rl = (t * 64 + 64 <= nrec ? t * 64 + 64 : nrec) - 1;  // the tile's last record
+    uint32_t nl = 0, nc = 0, ls = 0, na = 0;
+    uint64_t src = 0, o_name = 0, o_cig = 0, o_seq = 0, o_aux = 0;
+    if (r < nrec && c.layout_ok[r]) {
+      src = rec_off[r] + 36;
+      nl = c.name_len[r];
+      nc = c.cigar_n[r];
+      ls = c.seq_len[r];
+      na = c.aux_len[r];
+      o_name = c.name_off[r];
+      o_cig = c.cigar_off[r];
+      o_seq = c.seq_off[r];
+      o_aux = c.aux_off[r];
+    }
+    // the span every field of the tile lies in: [rec_off[first] + 36, rec_off[last] + 4 + bs)
+    const uint64_t lo = (rec_off[t * 64] + 36) & ~15ull;
+    const uint64_t hi = rec_off[rl] + 4 + (uint64_t)(uint32_t)c.block_size[rl];
+    const uint64_t span = hi > lo ? ((hi - lo + 15) & ~15ull) : 0;
+    const bool staged = span <= PL_BYTES;  // wave-uniform
+    if (staged) {
+      // 8 KiB per batch: eight loads per lane in flight, then their LDS stores (a lane past the
+      // span re-reads the span's first quad, so the loads need no branch)
+      constexpr uint32_t NQ = PL_BYTES / 1024;
+#pragma unroll
+      for (uint32_t k0 = 0; k0 < NQ; k0 += 8) {
+        if (1024u * k0 < span) {
+          uint4 q[8];
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t o = 1024u * (k0 + j) + 16u * lane;
+            q[j] = *(const uint4*)(u + lo + (o < span ? o : 0u));
+          }
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t o = 1024u * (k0 + j) + 16u * lane;
+            if (o < span) *(uint4*)(s_src + o) = q[j];
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t f = 0; f < 5; ++f) {
+      uint32_t len;
+      uint64_t s0, d0;
+      uint8_t* base;
+      if (f == 0) { len = nl; s0 = src; d0 = o_name; base = c.names; }
+      else if (f == 1) { len = 4u * nc; s0 = src + nl; d0 = 4 * o_cig; base = (uint8_t*)c.cigars; }
+      else if (f == 2) { len = ls; s0 = src + nl + 4u * nc; d0 = o_seq; base = c.seq; }
+      else if (f == 3) { len = ls; s0 = src + nl + 4u * nc + (ls + 1u) / 2u; d0 = o_seq; base = c.qual; }
+      else { len = na; s0 = src + nl + 4u * nc + (ls + 1u) / 2u + ls; d0 = o_aux; base = c.aux; }
+      const uint32_t units = (len + 15u) >> 4;
+      const uint32_t incl = wave_incl_sum(units, lane);
+      const uint32_t excl = incl - units;
+      const uint32_t total = __shfl(incl, 63);
+      for (uint32_t q0 = 0; q0 < total; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        uint32_t lo_l = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+          const uint32_t m = lo_l + step;
+          if (__shfl(excl, m) <= q) lo_l = m;
+        }
+        const uint32_t k = q - __shfl(excl, lo_l);
+        const uint32_t n = __shfl(len, lo_l) - 16u * k;
+        const uint64_t sq = __shfl(s0, lo_l), dq = __shfl(d0, lo_l);
+        if (q < total) {
+          uint8_t* dp = base + dq + 16u * k;
+          u32x4_a1 v;
+          if (staged) {
+            const uint32_t x = (uint32_t)(sq - lo);
+            v = f == 2 ? seq16_q(pl_rd8(s_src, x + 8u * k)) : pl_rd16(s_src, x + 16u * k);
+          } else {
+            v = f == 2 ? seq16(u + sq + 8u * k) : *(const u32x4_a1*)(u + sq + 16u * k);
+          }
+          if (n >= 16u) *(u32x4_a1*)dp = v;
+          else st_part(dp, n, v);
+        }
+      }
+    }
+    __syncthreads();  // the next tile's staging overwrites s_src
+  }
+}
+#endif
 
 // ------------------------------------------------------------------------------------
 // scans (u32 -> u64 exclusive), 3-phase reduce-then-scan

@@ -124,6 +124,12 @@ __device__ __forceinline__ uint64_t periodic8(uint64_t v, uint64_t sel) {
   return (uint64_t)r0 | (uint64_t)r1 << 32;
 }
 
+// 4 bytes at any LDS index x from two dword-aligned reads (a byte-aligned ds_read_b32 replays)
+__device__ __forceinline__ uint32_t lds_rd32u(const uint8_t* buf, uint32_t x) {
+  const uint32_t a = x & ~3u;
+  return __builtin_amdgcn_alignbit(*(const uint32_t*)(buf + a + 4u), *(const uint32_t*)(buf + a), (x & 3u) * 8u);
+}
+
 #ifdef HBAM_RS_ALIGNED
 // Every LDS access at its natural alignment (cdna_hip_programming.md Guideline 17: ds_read/write
 // _b64/_b128 off 8/16-byte alignment replay): bytes at any index are assembled from aligned
@@ -135,11 +141,7 @@ __device__ __forceinline__ uint32_t lw(const uint8_t* buf, uint32_t a) {  // a %
 __device__ __forceinline__ void lwr(uint8_t* buf, uint32_t a, uint32_t v) { *(uint32_t*)(buf + a) = v; }
 typedef uint32_t rs_u32a1 __attribute__((aligned(1)));
 typedef uint64_t rs_u64a1 __attribute__((aligned(1)));
-// 4 / 8 bytes at any index x
-__device__ __forceinline__ uint32_t lds_rd32u(const uint8_t* buf, uint32_t x) {
-  const uint32_t a = x & ~3u;
-  return __builtin_amdgcn_alignbit(lw(buf, a + 4u), lw(buf, a), (x & 3u) * 8u);
-}
+// 8 bytes at any index x
 __device__ __forceinline__ uint64_t lds_rd64u(const uint8_t* buf, uint32_t x) {
   const uint32_t a = x & ~3u, sh = (x & 3u) * 8u;
   const uint32_t w0 = lw(buf, a), w1 = lw(buf, a + 4u), w2 = lw(buf, a + 8u);

@@ -304,6 +304,8 @@ typedef struct hbam_sorted_run {
   uint64_t* offsets;
   uint8_t* payload;
 } hbam_sorted_run;
+/* device buffer of `bytes` bytes followed by 64 more readable bytes, so it may be passed back as a
+ * device-resident input (the 64-byte rule above); free with hbam_device_free */
 int hbam_device_alloc(hbam_ctx* ctx, uint64_t bytes, void** dev_out);
 /* the records of a decoded split (device columns) as a sorted run */
 int hbam_sort_split(hbam_ctx* ctx, const hbam_columns* dv, hbam_sorted_run* out);

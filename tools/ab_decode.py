@@ -29,6 +29,7 @@ d = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
 d[:len(data)].copy_(torch.from_numpy(data))
 d[len(data):].zero_()
 torch.cuda.synchronize()
+print("comp_bytes %d" % len(data), flush=True)
 digests = {}
 for lib in a.libs:
     _lib._LIB = None

@@ -4,10 +4,12 @@
 # Steps run in order, each under its own time limit, and the first one that fails hard (a
 # fault, an abort, a time limit) ends the call; pytest's "some tests failed" (rc 1) does not.
 #   tests[,EXPR]         pytest -m gpu (optionally -k EXPR)
+#   testslib,LIB[,EXPR] the same against hadoop-bam_amd/LIB (HBAM_LIB)
 #   smoke                __graft_entry__.smoke()
 #   bench[,STEPS]        python bench.py (default --steps 20 --warmup 3)
 #   prof                 rocprofv3 --kernel-trace --stats of a short bench.py run
 #   pmc,COUNTERS[,SIZE[,LIB]]  one rocprofv3 --pmc pass (COUNTERS separated by '+') over a decode
+#   pmcbytes[,SIZE]      FETCH_SIZE + WRITE_SIZE passes over a decode, folded by tools/pmc_summarize.py
 #   bin,PATH             run a probe executable (tools/probes/*)
 #   abdecode,SIZE,LIBS   tools/ab_decode.py A/B of library builds (LIBS separated by '+')
 #   stream,SIZE,WINDOW   tools/bench_stream.py (config #4 share)
@@ -30,6 +32,9 @@ for spec in "$@"; do
     tests)
       K=(); [ -n "$a1" ] && K=(-k "$a1")
       timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread "${K[@]}" > $O/tests.txt 2>&1; r=$? ;;
+    testslib)  # testslib,LIB[,EXPR]: pytest -m gpu against another build of the library
+      K=(); [ -n "$a2" ] && K=(-k "$a2")
+      HBAM_LIB=hadoop-bam_amd/$a1 timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread "${K[@]}" > $O/tests_$a1.txt 2>&1; r=$? ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1; r=$? ;;
     bench)
@@ -38,6 +43,14 @@ for spec in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --parity-splits 0 > $O/bench_prof.json 2> $O/prof.err; r=$? ;;
     pmc)  # pmc,COUNTERS[,SIZE[,LIB]]: one counter pass over a decode (csv per dispatch)
       timeout -s KILL 300 rocprofv3 --pmc ${a1//+/ } -d $O/pmc_${a1//+/_} -o run --output-format csv -- python3 tools/ab_decode.py --size ${a2:-2e9} --reps 1 --digest 0 --libs ${a3:-libhbam.so} > $O/pmc_${a1//+/_}.txt 2>&1; r=$? ;;
+    pmcbytes)  # pmcbytes[,SIZE]: FETCH_SIZE and WRITE_SIZE passes over one decode -> tools/pmc_summarize.py
+      timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmcb_fetch -o run --output-format csv -- python3 tools/ab_decode.py --size ${a1:-10e9} --reps 1 --digest 0 --libs libhbam.so > $O/pmcb_fetch.txt 2>&1 &&
+      timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d $O/pmcb_write -o run --output-format csv -- python3 tools/ab_decode.py --size ${a1:-10e9} --reps 1 --digest 0 --libs libhbam.so > $O/pmcb_write.txt 2>&1; r=$?
+      if [ $r -eq 0 ]; then
+        COMP=$(grep -m1 '^comp_bytes' $O/pmcb_fetch.txt | cut -d' ' -f2)
+        STG=""; [ -s $O/bench.json ] && STG=$O/bench.json
+        python3 tools/pmc_summarize.py $(ls $O/pmcb_fetch/*counter_collection.csv $O/pmcb_fetch/*/*counter_collection.csv 2>/dev/null | head -1) $(ls $O/pmcb_write/*counter_collection.csv $O/pmcb_write/*/*counter_collection.csv 2>/dev/null | head -1) $COMP $O/pmcsum round4 $STG > $O/pmcsum.txt 2>&1
+      fi ;;
     bin)  # bin,PATH: a probe executable of the repository
       timeout -k 10 300 ./$a1 > $O/$(basename $a1).txt 2>&1; r=$? ;;
     abdecode)

@@ -1,38 +1,84 @@
-"""Fold rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE) for one kernel into
-profiles/pmc_inflate.json, which bench.py reads as roofline.traffic.
+"""Fold two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; separate runs) over one decode into
+per-kernel HBM traffic, and the Huffman pass's entry that bench.py reads as roofline.traffic.
 
-Corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE
-are reported in KiB; on gfx950 FETCH_SIZE counts half the bytes of 16-B-per-lane reads, so it
-is doubled.  usage: pmc_summarize.py <fetch_csv> <write_csv> <kernel-substring> <comp_bytes> <out> [tree]
+Corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM section, checked on this repository's
+own access shapes by tools/pmc_calib.hip -> profiles/r04/calib/):
+  * FETCH_SIZE and WRITE_SIZE are reported in KiB;
+  * FETCH_SIZE counts 64 B per 128-B L2->fabric request, so it is doubled.  The guide states this
+    for 16-B-per-lane streaming reads; the calibration finds the same factor for every read shape
+    of the pipeline once bytes are counted as 128-B lines touched: streaming 16 B/lane 0.500
+    (model 0.5), 16-B units at +3 0.516, random 8-byte loads 8.41 per 8 B (model 16.96 / 2 = 8.48),
+    36-B fixed parts at stride 340 2.30 (model 4.53 / 2 = 2.27);
+  * WRITE_SIZE reads the bytes exactly (1.000 streaming, 1.152 for lane-per-64-KiB-region
+    16-byte stores: partial lines at region edges);
+  * FETCH counts L2 misses served by the 256 MiB Infinity Cache as well as HBM reads (guide,
+    HBM section).  When a kernel's corrected bytes over its time exceed the achievable 6.3 TB/s,
+    at least the excess came from the Infinity Cache: `hbm_bytes_max` caps the HBM share at
+    6.3 TB/s x time and `mall_bytes_min` is the rest.
+
+usage: pmc_summarize.py FETCH_CSV WRITE_CSV COMP_BYTES OUT_DIR TREE [STAGES_JSON]
+  STAGES_JSON: a bench.py line (its stages_ms give each kernel's unprofiled time)
+writes OUT_DIR/pmc_kernels.json (every kernel) and OUT_DIR/pmc_k_inflate_tokens.json (bench.py)
 """
 import csv
 import json
+import os
 import sys
 
+HBM_ACHIEVABLE = 6.3e12
+STAGE_OF = {"k_inflate_tokens": "huffman_ms", "k_resolve": "resolve_ms", "k_decode_pools": "pools_ms",
+            "k_decode_fixed": "decode_ms", "k_scan_chunks": "scan_ms"}
 
-def per_dispatch(path, kernel, counter):
+
+def per_kernel(path, counter):
+    """kernel -> list of per-dispatch values (KiB), summed over the counter's instances"""
     vals = {}
     for row in csv.DictReader(open(path)):
-        if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
-            vals[row["Dispatch_Id"]] = vals.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
+        if row["Counter_Name"] != counter:
+            continue
+        k = row["Kernel_Name"].split("(")[0].split("::")[-1].strip()
+        d = vals.setdefault(k, {})
+        d[row["Dispatch_Id"]] = d.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+    return {k: list(v.values()) for k, v in vals.items()}
 
 
 def main():
-    fcsv, wcsv, kern, comp, out = sys.argv[1:6]
-    tree = sys.argv[6] if len(sys.argv) > 6 else "round3"
-    f = per_dispatch(fcsv, kern, "FETCH_SIZE")
-    w = per_dispatch(wcsv, kern, "WRITE_SIZE")
-    assert f and w, "no dispatches of %s" % kern
-    # the decode of the whole file is the largest dispatch (smaller ones: header probe)
-    fetch = 2.0 * 1024.0 * max(f)
-    write = 1024.0 * max(w)
-    res = {"kernel": kern, "tree": tree, "comp_bytes": int(comp), "dispatches": [len(f), len(w)],
-           "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
-           "hbm_bytes_per_launch": fetch + write,
-           "note": "FETCH_SIZE x2 (gfx950 16-B/lane read correction), KiB -> B"}
-    json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps(res))
+    fcsv, wcsv, comp, outdir, tree = sys.argv[1:6]
+    stages = {}
+    if len(sys.argv) > 6:
+        stages = json.load(open(sys.argv[6])).get("stages_ms", {})
+    f = per_kernel(fcsv, "FETCH_SIZE")
+    w = per_kernel(wcsv, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(f) | set(w)):
+        # the decode of the whole file is the largest dispatch (smaller ones: header probe)
+        fetch = 2.0 * 1024.0 * max(f.get(k, [0.0]))
+        write = 1024.0 * max(w.get(k, [0.0]))
+        e = {"fetch_raw_kib": max(f.get(k, [0.0])), "write_raw_kib": max(w.get(k, [0.0])),
+             "fetch_bytes": fetch, "write_bytes": write, "hbm_bytes_per_launch": fetch + write}
+        ms = stages.get(STAGE_OF.get(k, ""), 0.0)
+        if ms:
+            t = ms / 1e3
+            e["ms"] = ms
+            e["implied_tb_s"] = round((fetch + write) / t / 1e12, 3)
+            cap = HBM_ACHIEVABLE * t
+            e["hbm_bytes_max"] = min(fetch + write, cap)
+            e["mall_bytes_min"] = max(0.0, fetch + write - cap)
+        res[k] = e
+    os.makedirs(outdir, exist_ok=True)
+    note = ("FETCH_SIZE x2 (128-B requests tallied at 64 B; calibrated per access shape: "
+            "profiles/r04/calib/), KiB -> B; FETCH includes Infinity Cache hits")
+    json.dump({"tree": tree, "comp_bytes": int(comp), "note": note, "kernels": res},
+              open(os.path.join(outdir, "pmc_kernels.json"), "w"), indent=1)
+    h = res.get("k_inflate_tokens")
+    if h:
+        one = {"kernel": "k_inflate_tokens", "tree": tree, "comp_bytes": int(comp),
+               "fetch_bytes_per_launch": h["fetch_bytes"], "write_bytes_per_launch": h["write_bytes"],
+               "hbm_bytes_per_launch": h["hbm_bytes_per_launch"], "note": note}
+        json.dump(one, open(os.path.join(outdir, "pmc_k_inflate_tokens.json"), "w"), indent=1)
+    for k, e in res.items():
+        print("%-24s fetch %8.2f GB write %8.2f GB%s" % (k, e["fetch_bytes"] / 1e9, e["write_bytes"] / 1e9,
+              ("  %.2f TB/s implied" % e["implied_tb_s"]) if "implied_tb_s" in e else ""))
 
 
 if __name__ == "__main__":
