@@ -340,10 +340,13 @@ __device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64
 #define HBAM_RS_WAVES 8
 #endif
 #ifndef HBAM_RS_DSC_AL
-#define HBAM_RS_DSC_AL 0
+#define HBAM_RS_DSC_AL 1  // aligned descriptor reads: 21.5 -> 21.0 ms at 5 GB (profiles/r04/ab/resolve_depmask_dscal_5g.txt)
+#endif
+#ifndef HBAM_RS_NT_RAW
+#define HBAM_RS_NT_RAW 0
 #endif
 #ifndef HBAM_RS_DEPMASK
-#define HBAM_RS_DEPMASK 0
+#define HBAM_RS_DEPMASK 1  // dependency masks for <= 64 ordered matches: 21.5 -> 19.6 ms; both 19.1 (same file)
 #endif
 __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* __restrict__ blk,
                                                 const uint64_t* __restrict__ uoff, uint32_t nblk,
@@ -396,8 +399,18 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
   auto load_raw = [&](uint32_t k, uint4& r0, uint4& r1) {
     const uint64_t g = abase + (uint64_t)k * RS_S + 16u * lane;
     if (k < nstr) {
+#if HBAM_RS_NT_RAW
+      // read once here (the stretch comes back through LDS and the write-back): no L2 allocation
+      const u32x4_t q0 = __builtin_nontemporal_load((const u32x4_t*)(ubuf + g));
+      r0 = make_uint4(q0[0], q0[1], q0[2], q0[3]);
+      if (RS_C == 2) {
+        const u32x4_t q1 = __builtin_nontemporal_load((const u32x4_t*)(ubuf + g + 1024));
+        r1 = make_uint4(q1[0], q1[1], q1[2], q1[3]);
+      }
+#else
       r0 = *(const uint4*)(ubuf + g);
       if (RS_C == 2) r1 = *(const uint4*)(ubuf + g + 1024);
+#endif
     }
   };
   uint4 ra0 = make_uint4(0, 0, 0, 0), ra1 = ra0, rb0 = ra0, rb1 = ra0;
@@ -501,6 +514,13 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
         rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
       } else {  // dist > RS_W >= 258 >= len: no overlap with the destination
         const uint32_t gl = (lds_from - src) < len ? (lds_from - src) : len;
+#if HBAM_RS_NT_FAR
+        // sources further back than HBAM_RS_NT_FAR bytes: loaded without L2 allocation, so they do
+        // not evict the recent lines most far matches read (k_resolve's L2 hit rate: 22 %,
+        // profiles/r04/pmc/tcc_2g.json)
+        if (s0 - src > HBAM_RS_NT_FAR) rs_copy_glb_nt(s_buf, lbase + p, gl, ubuf + base + src);
+        else
+#endif
         rs_copy_glb(s_buf, lbase + p, gl, ubuf + base + src);
         if (gl < len) rs_copy_lds(s_buf, lbase + p + gl, len - gl, dist, s_sel);
       }

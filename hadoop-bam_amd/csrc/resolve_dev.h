@@ -29,6 +29,9 @@ namespace hbam {
 // 42.6 ms (profiles/r02/s2/ab_resolve_occupancy_10g.txt); 0 is not supported
 #define HBAM_RS_W 512
 #endif
+#ifndef HBAM_RS_NT_FAR
+#define HBAM_RS_NT_FAR 0  // A/B: far sources further back than this many bytes loaded non-temporal
+#endif
 #ifndef HBAM_RS_S
 #define HBAM_RS_S 1024  // A/B at 2 GB (window 1 KiB): 2048 -> 16.8 ms, 1024 -> 11.7 ms
 #endif
@@ -292,6 +295,25 @@ __device__ __forceinline__ void rs_copy_glb(uint8_t* __restrict__ buf, uint32_t 
     // profiles/r03/ab/decode_fixed_hoist_and_resolve_g16_5g.txt)
     const uint64_t v0 = *(const uint64_t*)(g + t), v1 = *(const uint64_t*)(g + t + 8),
                    v2 = *(const uint64_t*)(g + t + 16), v3 = *(const uint64_t*)(g + t + 24);
+    const uint32_t n = len - t;
+    lds_wr_part(d + t, v0, n);
+    if (n > 8u) lds_wr_part(d + t + 8, v1, n - 8u);
+    if (n > 16u) lds_wr_part(d + t + 16, v2, n - 16u);
+    if (n > 24u) lds_wr_part(d + t + 24, v3, n - 24u);
+  }
+}
+#endif
+
+#if HBAM_RS_NT_FAR
+// rs_copy_glb with non-temporal 8-byte loads
+__device__ __forceinline__ void rs_copy_glb_nt(uint8_t* __restrict__ buf, uint32_t di, uint32_t len,
+                                               const uint8_t* __restrict__ g) {
+  uint8_t* d = buf + di;
+  for (uint32_t t = 0; t < len; t += 32u) {
+    const uint64_t v0 = __builtin_nontemporal_load((const uint64_t*)(g + t)),
+                   v1 = __builtin_nontemporal_load((const uint64_t*)(g + t + 8)),
+                   v2 = __builtin_nontemporal_load((const uint64_t*)(g + t + 16)),
+                   v3 = __builtin_nontemporal_load((const uint64_t*)(g + t + 24));
     const uint32_t n = len - t;
     lds_wr_part(d + t, v0, n);
     if (n > 8u) lds_wr_part(d + t + 8, v1, n - 8u);
