@@ -342,6 +342,9 @@ __device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64
 #ifndef HBAM_RS_DSC_AL
 #define HBAM_RS_DSC_AL 1  // aligned descriptor reads: 21.5 -> 21.0 ms at 5 GB (profiles/r04/ab/resolve_depmask_dscal_5g.txt)
 #endif
+#ifndef HBAM_RS_MERGE
+#define HBAM_RS_MERGE 0
+#endif
 #ifndef HBAM_RS_NT_RAW
 #define HBAM_RS_NT_RAW 0
 #endif
@@ -452,6 +455,67 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
       }
     }
     __syncthreads();
+#if HBAM_RS_MERGE
+    // ---- descriptors, with the pre matches copied on the spot.  A pre match (source ending
+    // before the stretch: every source byte final) is copied by the lane that read its
+    // descriptor, in the same step: no record list, no second pass.  Only the ordered matches
+    // are listed (packed with their stretch-relative start: an ordered match's distance is
+    // < 1,281, so p - s0 | len-3 | dist-1 fit in 29 bits and need no position lookup).  A copy
+    // writes only its own hole, which holds no other match's descriptor, so later steps still
+    // read theirs intact.  LDS holds block offsets from s0 - RS_W - a0; a source older than that
+    // is read from ubuf (stretches <= k-2, written back at least one iteration ago: the drain),
+    // and a source that straddles the boundary is copied in two parts.
+    if (s0 >= RS_W) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t lds_from = s0 - RS_W - a0;  // block offset of LDS index 0 (when s0 >= RS_W)
+    uint32_t nord = 0;
+    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      uint32_t p = 0, len = 0, dist = 0;
+      bool pre = false, ord = false, bad = false;
+      if (j < total) {
+        p = s_pos[j];
+        const uint32_t dsc = lds_rd32u(s_buf, lbase + p);
+        len = (dsc & 0xffu) + 3u;
+        dist = ((dsc >> 8) & 0xffffu) + 1u;
+        const uint32_t e = p - dist + (len < dist ? len : dist);
+        // a descriptor the Huffman pass cannot have written (source before the block, or a
+        // hole past the block end): the block's tokens are corrupt
+        bad = dist > p || p + len > isize || dist > 32768u;
+        pre = !bad && e <= s0;
+        ord = !bad && !pre;
+      }
+      if (__any(bad)) {  // never copy from outside the block: report DataFormatException
+        if (lane == 0) status[b] = INF_DATA;
+        return;
+      }
+      if (pre) {
+        const uint32_t src = p - dist;
+        if (src + RS_W + a0 >= s0) {
+          rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
+        } else {  // dist > RS_W >= 258 >= len: no overlap with the destination
+          const uint32_t gl = (lds_from - src) < len ? (lds_from - src) : len;
+          rs_copy_glb(s_buf, lbase + p, gl, ubuf + base + src);
+          if (gl < len) rs_copy_lds(s_buf, lbase + p + gl, len - gl, dist, s_sel);
+        }
+      }
+      const uint64_t mo = __ballot(ord);
+      if (ord) s_rec[RS_MAXM - 1 - (nord + lane_rank(mo))] = (p - s0) | (len - 3u) << 10 | (dist - 1u) << 18;
+      nord += (uint32_t)__popcll(mo);
+    }
+    __syncthreads();
+#ifdef HBAM_PROF
+    const uint64_t q1 = PROF_CLK();
+    p_desc += q1 - q0;
+    n_m += total;
+#endif
+    // ordered record -> p | len << 16 | dist << 32 | e << 48 (the rs_unpack layout)
+    auto unpack_o = [&](uint32_t pk) -> uint64_t {
+      const uint32_t p = s0 + (pk & 1023u), len = ((pk >> 10) & 255u) + 3u, dist = (pk >> 18) + 1u;
+      const uint32_t e = p - dist + (len < dist ? len : dist);
+      return (uint64_t)p | (uint64_t)len << 16 | (uint64_t)dist << 32 | (uint64_t)e << 48;
+    };
+#define HBAM_RS_UNPACK_ORD(pk) unpack_o(pk)
+#else
     // ---- descriptors -> records, split pre / ordered
     uint32_t npre = 0, nord = 0;
     bool bad_desc = false;
@@ -528,6 +592,8 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
 #ifdef HBAM_PROF
     p_pre += PROF_CLK() - q1;
 #endif
+#define HBAM_RS_UNPACK_ORD(pk) rs_unpack(pk, s_pos)
+#endif
     // ---- ordered matches: dataflow rounds.  s_pend holds one bit per byte of the stretch
     // (+ match spill) that an ordered match has yet to write; a match is ready when no byte of
     // its external source [p - dist, p - dist + min(len, dist)) is pending.  Every round
@@ -541,7 +607,7 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
       // [lo, hi): lo = #{k': end(k') <= a}, hi = #{k': p(k') < e} (< k).  A round is then a
       // compare against the wave-uniform done mask and the copies: no LDS state besides the bytes.
       const bool mine = lane < nord;
-      const uint64_t rec = mine ? rs_unpack(s_rec[RS_MAXM - 1 - lane], s_pos) : 0ull;
+      const uint64_t rec = mine ? HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - lane]) : 0ull;
       const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
                      dist = (uint32_t)(rec >> 32) & 0xffffu, e = (uint32_t)(rec >> 48);
       const uint32_t a = p - dist;
@@ -578,11 +644,11 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
       // slots would cost the kernel half its occupancy)
       const uint32_t mine = nord > lane ? (nord - lane + 63u) / 64u : 0u;
       uint32_t live = mine >= 32u ? ~0u : (1u << mine) - 1u;
-      const uint64_t rec0 = mine ? rs_unpack(s_rec[RS_MAXM - 1 - lane], s_pos) : 0ull;
+      const uint64_t rec0 = mine ? HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - lane]) : 0ull;
       if (mine) rs_bits(s_pend, ((uint32_t)rec0 & 0xffffu) - s0, (uint32_t)(rec0 >> 16) & 0xffffu, true);
 #pragma unroll 1
       for (uint32_t t = 1; t < mine; ++t) {
-        const uint64_t rec = rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos);
+        const uint64_t rec = HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - (lane + 64u * t)]);
         rs_bits(s_pend, ((uint32_t)rec & 0xffffu) - s0, (uint32_t)(rec >> 16) & 0xffffu, true);
       }
       rs_lds_order();
@@ -603,12 +669,12 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
         uint32_t ready = (live & 1u) && is_ready(rec0) ? 1u : 0u;
 #pragma unroll 1
         for (uint32_t t = 1; t < mine; ++t)
-          if ((live >> t & 1u) && is_ready(rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos))) ready |= 1u << t;
+          if ((live >> t & 1u) && is_ready(HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - (lane + 64u * t)]))) ready |= 1u << t;
         rs_lds_order();
         if (ready & 1u) run(rec0);
 #pragma unroll 1
         for (uint32_t t = 1; t < mine; ++t)
-          if (ready >> t & 1u) run(rs_unpack(s_rec[RS_MAXM - 1 - (lane + 64u * t)], s_pos));
+          if (ready >> t & 1u) run(HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - (lane + 64u * t)]));
         live &= ~ready;
 #ifdef HBAM_PROF
         ++n_bat;
@@ -1203,6 +1269,104 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
     }
   }
 }
+
+#ifdef HBAM_POOLS_PIPE
+// A/B variant of k_decode_pools with the next unit's load issued before this unit's store.
+// In k_decode_pools every step waits `vmcnt(0)`: on CDNA vmcnt counts stores too and memory
+// operations retire in issue order, so waiting for a load issued after a store waits for the
+// store's acknowledgement as well, and the partial-unit pieces (stores under exec-mask branches)
+// leave the compiler no static count, so it drains.  Here a field's whole 16-byte units run in a
+// loop with exactly one load (the next step's, issued first) and one store per step -- a lane
+// with nothing to store writes its slot of a 1 KiB dummy line -- so the wait before a store is
+// vmcnt(1): the previous store stays in flight.  The last, partial unit of each record's field
+// is then written by the record's own lane (one load, the pieces), no search needed.
+static __device__ __forceinline__ u32x4_a1 seq16_w(uint32_t lo, uint32_t hi) {
+  const uint64_t q = (uint64_t)lo | (uint64_t)hi << 32;
+  u32x4_a1 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = seq4((uint32_t)(q >> (16 * j)) & 0xffu, (uint32_t)(q >> (16 * j + 8)) & 0xffu);
+  return o;
+}
+__global__ __launch_bounds__(256) void k_decode_pools_pipe(const uint8_t* __restrict__ u, uint64_t nrec,
+                                                          const uint64_t* __restrict__ rec_off,
+                                                          DevColumns c, uint8_t* __restrict__ dummy) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t ntiles = (nrec + 63) / 64;
+  const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
+  uint8_t* const my_dummy = dummy + 16u * lane;
+  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); t < ntiles; t += wstride) {
+    const uint64_t r = t * 64 + lane;
+    uint32_t nl = 0, nc = 0, ls = 0, na = 0;
+    uint64_t src = 0, o_name = 0, o_cig = 0, o_seq = 0, o_aux = 0;
+    if (r < nrec && c.layout_ok[r]) {
+      src = rec_off[r] + 36;
+      nl = c.name_len[r];
+      nc = c.cigar_n[r];
+      ls = c.seq_len[r];
+      na = c.aux_len[r];
+      o_name = c.name_off[r];
+      o_cig = c.cigar_off[r];
+      o_seq = c.seq_off[r];
+      o_aux = c.aux_off[r];
+    }
+#pragma unroll 1
+    for (uint32_t f = 0; f < 5; ++f) {
+      uint32_t len;
+      uint64_t s0, d0;
+      uint8_t* base;
+      if (f == 0) { len = nl; s0 = src; d0 = o_name; base = c.names; }
+      else if (f == 1) { len = 4u * nc; s0 = src + nl; d0 = 4 * o_cig; base = (uint8_t*)c.cigars; }
+      else if (f == 2) { len = ls; s0 = src + nl + 4u * nc; d0 = o_seq; base = c.seq; }
+      else if (f == 3) { len = ls; s0 = src + nl + 4u * nc + (ls + 1u) / 2u; d0 = o_seq; base = c.qual; }
+      else { len = na; s0 = src + nl + 4u * nc + (ls + 1u) / 2u + ls; d0 = o_aux; base = c.aux; }
+      const uint32_t sstep = f == 2 ? 8u : 16u;  // source bytes per unit
+      const uint32_t full = len >> 4;
+      const uint32_t incl = wave_incl_sum(full, lane);
+      const uint32_t excl = incl - full;
+      const uint32_t total = __shfl(incl, 63);
+      // full unit q -> source / destination (all 64 lanes take part in the shuffles); a lane past
+      // the last unit reads byte 0 and stores to its dummy slot
+      auto locate = [&](uint32_t q, const uint8_t*& sp, uint8_t*& dp) {
+        uint32_t lo = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+          const uint32_t m = lo + step;
+          if (__shfl(excl, m) <= q) lo = m;
+        }
+        const uint32_t k = q - __shfl(excl, lo);
+        const uint64_t sq = __shfl(s0, lo), dq = __shfl(d0, lo);
+        const bool ok = q < total;
+        sp = ok ? u + sq + sstep * k : u;
+        dp = ok ? base + dq + 16u * k : my_dummy;
+      };
+      if (total) {
+        // two register sets in turn (a loop-carried copy would make the compiler wait for the
+        // load just issued at the end of each step)
+        const uint8_t* sp;
+        uint8_t *da, *db;
+        locate(lane, sp, da);
+        u32x4_a1 va = *(const u32x4_a1*)sp, vb;
+        for (uint32_t q0 = 0;; q0 += 128) {
+          locate(q0 + 64 + lane, sp, db);
+          vb = *(const u32x4_a1*)sp;
+          *(u32x4_a1*)da = f == 2 ? seq16_w(va[0], va[1]) : va;
+          if (q0 + 64 >= total) break;
+          locate(q0 + 128 + lane, sp, da);
+          va = *(const u32x4_a1*)sp;
+          *(u32x4_a1*)db = f == 2 ? seq16_w(vb[0], vb[1]) : vb;
+          if (q0 + 128 >= total) break;
+        }
+      }
+      // the record's partial last unit (its own lane)
+      const uint32_t rem = len & 15u;
+      if (rem) {
+        const u32x4_a1 v = *(const u32x4_a1*)(u + s0 + sstep * full);
+        st_part(base + d0 + 16u * full, rem, f == 2 ? seq16_w(v[0], v[1]) : v);
+      }
+    }
+  }
+}
+#endif
 
 #ifdef HBAM_POOLS_LDS
 // A/B variant: the tile's record bytes staged in LDS first.  k_decode_pools waits for one
