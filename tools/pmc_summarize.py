@@ -36,7 +36,9 @@ def per_kernel(path, counter):
     for row in csv.DictReader(open(path)):
         if row["Counter_Name"] != counter:
             continue
-        k = row["Kernel_Name"].split("(")[0].split("::")[-1].strip()
+        k = row["Kernel_Name"].split("(")[0].strip()
+        k = k[5:] if k.startswith("void ") else k
+        k = k[6:] if k.startswith("hbam::") else k
         d = vals.setdefault(k, {})
         d[row["Dispatch_Id"]] = d.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
     return {k: list(v.values()) for k, v in vals.items()}
