@@ -175,7 +175,6 @@ enum BufId {
   B_G_OOFF,
   B_G_BS,
   B_G_PAY,
-  B_POOLS_DUMMY,  // k_decode_pools_pipe: per-lane slots for stores with nothing to write
   B_COUNT_ALL
 };
 
@@ -1155,21 +1154,9 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if ((rc = ensure(c, B_C_QUAL, tot_seq + 1, &dc.qual))) return rc;
   if ((rc = ensure(c, B_C_AUX, tot_aux + 1, &dc.aux))) return rc;
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
-#if defined(HBAM_POOLS_PIPE)
-  uint8_t* pdummy;
-  if ((rc = ensure(c, B_POOLS_DUMMY, 1024, &pdummy))) return rc;
-  if (n_final)
-    k_decode_pools_pipe<<<(uint32_t)std::min<uint64_t>(grid_for(n_final, 256), POOLS_MAX_WG), 256, 0, c->stream>>>(
-        ub, n_final, rec_off, dc, pdummy);
-#elif defined(HBAM_POOLS_LDS)
-  if (n_final)
-    k_decode_pools_lds<<<(uint32_t)std::min<uint64_t>((n_final + 63) / 64, 6144), 64, 0, c->stream>>>(
-        ub, n_final, rec_off, dc);
-#else
   if (n_final)
     k_decode_pools<<<(uint32_t)std::min<uint64_t>(grid_for(n_final, 256), POOLS_MAX_WG), 256, 0, c->stream>>>(
         ub, n_final, rec_off, dc);
-#endif
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

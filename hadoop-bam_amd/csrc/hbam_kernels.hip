@@ -342,12 +342,6 @@ __device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64
 #ifndef HBAM_RS_DSC_AL
 #define HBAM_RS_DSC_AL 1  // aligned descriptor reads: 21.5 -> 21.0 ms at 5 GB (profiles/r04/ab/resolve_depmask_dscal_5g.txt)
 #endif
-#ifndef HBAM_RS_MERGE
-#define HBAM_RS_MERGE 0
-#endif
-#ifndef HBAM_RS_NT_RAW
-#define HBAM_RS_NT_RAW 0
-#endif
 #ifndef HBAM_RS_DEPMASK
 #define HBAM_RS_DEPMASK 1  // dependency masks for <= 64 ordered matches: 21.5 -> 19.6 ms; both 19.1 (same file)
 #endif
@@ -402,18 +396,8 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
   auto load_raw = [&](uint32_t k, uint4& r0, uint4& r1) {
     const uint64_t g = abase + (uint64_t)k * RS_S + 16u * lane;
     if (k < nstr) {
-#if HBAM_RS_NT_RAW
-      // read once here (the stretch comes back through LDS and the write-back): no L2 allocation
-      const u32x4_t q0 = __builtin_nontemporal_load((const u32x4_t*)(ubuf + g));
-      r0 = make_uint4(q0[0], q0[1], q0[2], q0[3]);
-      if (RS_C == 2) {
-        const u32x4_t q1 = __builtin_nontemporal_load((const u32x4_t*)(ubuf + g + 1024));
-        r1 = make_uint4(q1[0], q1[1], q1[2], q1[3]);
-      }
-#else
       r0 = *(const uint4*)(ubuf + g);
       if (RS_C == 2) r1 = *(const uint4*)(ubuf + g + 1024);
-#endif
     }
   };
   uint4 ra0 = make_uint4(0, 0, 0, 0), ra1 = ra0, rb0 = ra0, rb1 = ra0;
@@ -455,67 +439,6 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
       }
     }
     __syncthreads();
-#if HBAM_RS_MERGE
-    // ---- descriptors, with the pre matches copied on the spot.  A pre match (source ending
-    // before the stretch: every source byte final) is copied by the lane that read its
-    // descriptor, in the same step: no record list, no second pass.  Only the ordered matches
-    // are listed (packed with their stretch-relative start: an ordered match's distance is
-    // < 1,281, so p - s0 | len-3 | dist-1 fit in 29 bits and need no position lookup).  A copy
-    // writes only its own hole, which holds no other match's descriptor, so later steps still
-    // read theirs intact.  LDS holds block offsets from s0 - RS_W - a0; a source older than that
-    // is read from ubuf (stretches <= k-2, written back at least one iteration ago: the drain),
-    // and a source that straddles the boundary is copied in two parts.
-    if (s0 >= RS_W) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t lds_from = s0 - RS_W - a0;  // block offset of LDS index 0 (when s0 >= RS_W)
-    uint32_t nord = 0;
-    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      uint32_t p = 0, len = 0, dist = 0;
-      bool pre = false, ord = false, bad = false;
-      if (j < total) {
-        p = s_pos[j];
-        const uint32_t dsc = lds_rd32u(s_buf, lbase + p);
-        len = (dsc & 0xffu) + 3u;
-        dist = ((dsc >> 8) & 0xffffu) + 1u;
-        const uint32_t e = p - dist + (len < dist ? len : dist);
-        // a descriptor the Huffman pass cannot have written (source before the block, or a
-        // hole past the block end): the block's tokens are corrupt
-        bad = dist > p || p + len > isize || dist > 32768u;
-        pre = !bad && e <= s0;
-        ord = !bad && !pre;
-      }
-      if (__any(bad)) {  // never copy from outside the block: report DataFormatException
-        if (lane == 0) status[b] = INF_DATA;
-        return;
-      }
-      if (pre) {
-        const uint32_t src = p - dist;
-        if (src + RS_W + a0 >= s0) {
-          rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
-        } else {  // dist > RS_W >= 258 >= len: no overlap with the destination
-          const uint32_t gl = (lds_from - src) < len ? (lds_from - src) : len;
-          rs_copy_glb(s_buf, lbase + p, gl, ubuf + base + src);
-          if (gl < len) rs_copy_lds(s_buf, lbase + p + gl, len - gl, dist, s_sel);
-        }
-      }
-      const uint64_t mo = __ballot(ord);
-      if (ord) s_rec[RS_MAXM - 1 - (nord + lane_rank(mo))] = (p - s0) | (len - 3u) << 10 | (dist - 1u) << 18;
-      nord += (uint32_t)__popcll(mo);
-    }
-    __syncthreads();
-#ifdef HBAM_PROF
-    const uint64_t q1 = PROF_CLK();
-    p_desc += q1 - q0;
-    n_m += total;
-#endif
-    // ordered record -> p | len << 16 | dist << 32 | e << 48 (the rs_unpack layout)
-    auto unpack_o = [&](uint32_t pk) -> uint64_t {
-      const uint32_t p = s0 + (pk & 1023u), len = ((pk >> 10) & 255u) + 3u, dist = (pk >> 18) + 1u;
-      const uint32_t e = p - dist + (len < dist ? len : dist);
-      return (uint64_t)p | (uint64_t)len << 16 | (uint64_t)dist << 32 | (uint64_t)e << 48;
-    };
-#define HBAM_RS_UNPACK_ORD(pk) unpack_o(pk)
-#else
     // ---- descriptors -> records, split pre / ordered
     uint32_t npre = 0, nord = 0;
     bool bad_desc = false;
@@ -578,13 +501,6 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
         rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
       } else {  // dist > RS_W >= 258 >= len: no overlap with the destination
         const uint32_t gl = (lds_from - src) < len ? (lds_from - src) : len;
-#if HBAM_RS_NT_FAR
-        // sources further back than HBAM_RS_NT_FAR bytes: loaded without L2 allocation, so they do
-        // not evict the recent lines most far matches read (k_resolve's L2 hit rate: 22 %,
-        // profiles/r04/pmc/tcc_2g.json)
-        if (s0 - src > HBAM_RS_NT_FAR) rs_copy_glb_nt(s_buf, lbase + p, gl, ubuf + base + src);
-        else
-#endif
         rs_copy_glb(s_buf, lbase + p, gl, ubuf + base + src);
         if (gl < len) rs_copy_lds(s_buf, lbase + p + gl, len - gl, dist, s_sel);
       }
@@ -593,7 +509,6 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
     p_pre += PROF_CLK() - q1;
 #endif
 #define HBAM_RS_UNPACK_ORD(pk) rs_unpack(pk, s_pos)
-#endif
     // ---- ordered matches: dataflow rounds.  s_pend holds one bit per byte of the stretch
     // (+ match spill) that an ordered match has yet to write; a match is ready when no byte of
     // its external source [p - dist, p - dist + min(len, dist)) is pending.  Every round
@@ -1269,232 +1184,6 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
     }
   }
 }
-
-#ifdef HBAM_POOLS_PIPE
-// A/B variant of k_decode_pools with the next unit's load issued before this unit's store.
-// In k_decode_pools every step waits `vmcnt(0)`: on CDNA vmcnt counts stores too and memory
-// operations retire in issue order, so waiting for a load issued after a store waits for the
-// store's acknowledgement as well, and the partial-unit pieces (stores under exec-mask branches)
-// leave the compiler no static count, so it drains.  Here a field's whole 16-byte units run in a
-// loop with exactly one load (the next step's, issued first) and one store per step -- a lane
-// with nothing to store writes its slot of a 1 KiB dummy line -- so the wait before a store is
-// vmcnt(1): the previous store stays in flight.  The last, partial unit of each record's field
-// is then written by the record's own lane (one load, the pieces), no search needed.
-static __device__ __forceinline__ u32x4_a1 seq16_w(uint32_t lo, uint32_t hi) {
-  const uint64_t q = (uint64_t)lo | (uint64_t)hi << 32;
-  u32x4_a1 o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = seq4((uint32_t)(q >> (16 * j)) & 0xffu, (uint32_t)(q >> (16 * j + 8)) & 0xffu);
-  return o;
-}
-__global__ __launch_bounds__(256) void k_decode_pools_pipe(const uint8_t* __restrict__ u, uint64_t nrec,
-                                                          const uint64_t* __restrict__ rec_off,
-                                                          DevColumns c, uint8_t* __restrict__ dummy) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t ntiles = (nrec + 63) / 64;
-  const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
-  uint8_t* const my_dummy = dummy + 16u * lane;
-  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); t < ntiles; t += wstride) {
-    const uint64_t r = t * 64 + lane;
-    uint32_t nl = 0, nc = 0, ls = 0, na = 0;
-    uint64_t src = 0, o_name = 0, o_cig = 0, o_seq = 0, o_aux = 0;
-    if (r < nrec && c.layout_ok[r]) {
-      src = rec_off[r] + 36;
-      nl = c.name_len[r];
-      nc = c.cigar_n[r];
-      ls = c.seq_len[r];
-      na = c.aux_len[r];
-      o_name = c.name_off[r];
-      o_cig = c.cigar_off[r];
-      o_seq = c.seq_off[r];
-      o_aux = c.aux_off[r];
-    }
-#pragma unroll 1
-    for (uint32_t f = 0; f < 5; ++f) {
-      uint32_t len;
-      uint64_t s0, d0;
-      uint8_t* base;
-      if (f == 0) { len = nl; s0 = src; d0 = o_name; base = c.names; }
-      else if (f == 1) { len = 4u * nc; s0 = src + nl; d0 = 4 * o_cig; base = (uint8_t*)c.cigars; }
-      else if (f == 2) { len = ls; s0 = src + nl + 4u * nc; d0 = o_seq; base = c.seq; }
-      else if (f == 3) { len = ls; s0 = src + nl + 4u * nc + (ls + 1u) / 2u; d0 = o_seq; base = c.qual; }
-      else { len = na; s0 = src + nl + 4u * nc + (ls + 1u) / 2u + ls; d0 = o_aux; base = c.aux; }
-      const uint32_t sstep = f == 2 ? 8u : 16u;  // source bytes per unit
-      const uint32_t full = len >> 4;
-      const uint32_t incl = wave_incl_sum(full, lane);
-      const uint32_t excl = incl - full;
-      const uint32_t total = __shfl(incl, 63);
-      // full unit q -> source / destination (all 64 lanes take part in the shuffles); a lane past
-      // the last unit reads byte 0 and stores to its dummy slot
-      auto locate = [&](uint32_t q, const uint8_t*& sp, uint8_t*& dp) {
-        uint32_t lo = 0;
-#pragma unroll
-        for (uint32_t step = 32; step; step >>= 1) {
-          const uint32_t m = lo + step;
-          if (__shfl(excl, m) <= q) lo = m;
-        }
-        const uint32_t k = q - __shfl(excl, lo);
-        const uint64_t sq = __shfl(s0, lo), dq = __shfl(d0, lo);
-        const bool ok = q < total;
-        sp = ok ? u + sq + sstep * k : u;
-        dp = ok ? base + dq + 16u * k : my_dummy;
-      };
-      if (total) {
-        // two register sets in turn (a loop-carried copy would make the compiler wait for the
-        // load just issued at the end of each step)
-        const uint8_t* sp;
-        uint8_t *da, *db;
-        locate(lane, sp, da);
-        u32x4_a1 va = *(const u32x4_a1*)sp, vb;
-        for (uint32_t q0 = 0;; q0 += 128) {
-          locate(q0 + 64 + lane, sp, db);
-          vb = *(const u32x4_a1*)sp;
-          *(u32x4_a1*)da = f == 2 ? seq16_w(va[0], va[1]) : va;
-          if (q0 + 64 >= total) break;
-          locate(q0 + 128 + lane, sp, da);
-          va = *(const u32x4_a1*)sp;
-          *(u32x4_a1*)db = f == 2 ? seq16_w(vb[0], vb[1]) : vb;
-          if (q0 + 128 >= total) break;
-        }
-      }
-      // the record's partial last unit (its own lane)
-      const uint32_t rem = len & 15u;
-      if (rem) {
-        const u32x4_a1 v = *(const u32x4_a1*)(u + s0 + sstep * full);
-        st_part(base + d0 + 16u * full, rem, f == 2 ? seq16_w(v[0], v[1]) : v);
-      }
-    }
-  }
-}
-#endif
-
-#ifdef HBAM_POOLS_LDS
-// A/B variant: the tile's record bytes staged in LDS first.  k_decode_pools waits for one
-// 16-byte load per lane per unit step (one load in flight per wave: latency-bound, 80 % of wave
-// time parked); here the wave first copies the tile's whole source span ([first record's variable
-// part, last record's end), 16-byte aligned) into LDS with every load of the span in flight at
-// once, then numbers the units as above and reads them from LDS (aligned dwords + v_alignbit),
-// so only the stores touch HBM in the unit loop.  A tile whose span exceeds the LDS budget takes
-// the global path of k_decode_pools.
-#ifndef HBAM_POOLS_LDS_BYTES
-#define HBAM_POOLS_LDS_BYTES 24576
-#endif
-constexpr uint32_t PL_BYTES = HBAM_POOLS_LDS_BYTES;
-static __device__ __forceinline__ uint32_t pl_w(const uint8_t* s, uint32_t a) { return *(const uint32_t*)(s + a); }
-// 16 bytes at any LDS index x (reads up to x + 20)
-static __device__ __forceinline__ u32x4_a1 pl_rd16(const uint8_t* s, uint32_t x) {
-  const uint32_t a = x & ~3u, sh = (x & 3u) * 8u;
-  const uint32_t w0 = pl_w(s, a), w1 = pl_w(s, a + 4), w2 = pl_w(s, a + 8), w3 = pl_w(s, a + 12), w4 = pl_w(s, a + 16);
-  u32x4_a1 o;
-  o[0] = __builtin_amdgcn_alignbit(w1, w0, sh);
-  o[1] = __builtin_amdgcn_alignbit(w2, w1, sh);
-  o[2] = __builtin_amdgcn_alignbit(w3, w2, sh);
-  o[3] = __builtin_amdgcn_alignbit(w4, w3, sh);
-  return o;
-}
-static __device__ __forceinline__ uint64_t pl_rd8(const uint8_t* s, uint32_t x) {
-  const uint32_t a = x & ~3u, sh = (x & 3u) * 8u;
-  const uint32_t w0 = pl_w(s, a), w1 = pl_w(s, a + 4), w2 = pl_w(s, a + 8);
-  return (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) | (uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32;
-}
-static __device__ __forceinline__ u32x4_a1 seq16_q(uint64_t q) {
-  u32x4_a1 o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = seq4((uint32_t)(q >> (16 * j)) & 0xffu, (uint32_t)(q >> (16 * j + 8)) & 0xffu);
-  return o;
-}
-__global__ __launch_bounds__(64) void k_decode_pools_lds(const uint8_t* __restrict__ u, uint64_t nrec,
-                                                         const uint64_t* __restrict__ rec_off,
-                                                         DevColumns c) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_src[PL_BYTES + 32];
-  const uint32_t lane = threadIdx.x;
-  const uint64_t ntiles = (nrec + 63) / 64;
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint64_t r = t * 64 + lane;
-    const uint64_t rl = (t * 64 + 64 <= nrec ? t * 64 + 64 : nrec) - 1;  // the tile's last record
-    uint32_t nl = 0, nc = 0, ls = 0, na = 0;
-    uint64_t src = 0, o_name = 0, o_cig = 0, o_seq = 0, o_aux = 0;
-    if (r < nrec && c.layout_ok[r]) {
-      src = rec_off[r] + 36;
-      nl = c.name_len[r];
-      nc = c.cigar_n[r];
-      ls = c.seq_len[r];
-      na = c.aux_len[r];
-      o_name = c.name_off[r];
-      o_cig = c.cigar_off[r];
-      o_seq = c.seq_off[r];
-      o_aux = c.aux_off[r];
-    }
-    // the span every field of the tile lies in: [rec_off[first] + 36, rec_off[last] + 4 + bs)
-    const uint64_t lo = (rec_off[t * 64] + 36) & ~15ull;
-    const uint64_t hi = rec_off[rl] + 4 + (uint64_t)(uint32_t)c.block_size[rl];
-    const uint64_t span = hi > lo ? ((hi - lo + 15) & ~15ull) : 0;
-    const bool staged = span <= PL_BYTES;  // wave-uniform
-    if (staged) {
-      // 8 KiB per batch: eight loads per lane in flight, then their LDS stores (a lane past the
-      // span re-reads the span's first quad, so the loads need no branch)
-      constexpr uint32_t NQ = PL_BYTES / 1024;
-#pragma unroll
-      for (uint32_t k0 = 0; k0 < NQ; k0 += 8) {
-        if (1024u * k0 < span) {
-          uint4 q[8];
-#pragma unroll
-          for (uint32_t j = 0; j < 8; ++j) {
-            const uint32_t o = 1024u * (k0 + j) + 16u * lane;
-            q[j] = *(const uint4*)(u + lo + (o < span ? o : 0u));
-          }
-#pragma unroll
-          for (uint32_t j = 0; j < 8; ++j) {
-            const uint32_t o = 1024u * (k0 + j) + 16u * lane;
-            if (o < span) *(uint4*)(s_src + o) = q[j];
-          }
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (uint32_t f = 0; f < 5; ++f) {
-      uint32_t len;
-      uint64_t s0, d0;
-      uint8_t* base;
-      if (f == 0) { len = nl; s0 = src; d0 = o_name; base = c.names; }
-      else if (f == 1) { len = 4u * nc; s0 = src + nl; d0 = 4 * o_cig; base = (uint8_t*)c.cigars; }
-      else if (f == 2) { len = ls; s0 = src + nl + 4u * nc; d0 = o_seq; base = c.seq; }
-      else if (f == 3) { len = ls; s0 = src + nl + 4u * nc + (ls + 1u) / 2u; d0 = o_seq; base = c.qual; }
-      else { len = na; s0 = src + nl + 4u * nc + (ls + 1u) / 2u + ls; d0 = o_aux; base = c.aux; }
-      const uint32_t units = (len + 15u) >> 4;
-      const uint32_t incl = wave_incl_sum(units, lane);
-      const uint32_t excl = incl - units;
-      const uint32_t total = __shfl(incl, 63);
-      for (uint32_t q0 = 0; q0 < total; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        uint32_t lo_l = 0;
-#pragma unroll
-        for (uint32_t step = 32; step; step >>= 1) {
-          const uint32_t m = lo_l + step;
-          if (__shfl(excl, m) <= q) lo_l = m;
-        }
-        const uint32_t k = q - __shfl(excl, lo_l);
-        const uint32_t n = __shfl(len, lo_l) - 16u * k;
-        const uint64_t sq = __shfl(s0, lo_l), dq = __shfl(d0, lo_l);
-        if (q < total) {
-          uint8_t* dp = base + dq + 16u * k;
-          u32x4_a1 v;
-          if (staged) {
-            const uint32_t x = (uint32_t)(sq - lo);
-            v = f == 2 ? seq16_q(pl_rd8(s_src, x + 8u * k)) : pl_rd16(s_src, x + 16u * k);
-          } else {
-            v = f == 2 ? seq16(u + sq + 8u * k) : *(const u32x4_a1*)(u + sq + 16u * k);
-          }
-          if (n >= 16u) *(u32x4_a1*)dp = v;
-          else st_part(dp, n, v);
-        }
-      }
-    }
-    __syncthreads();  // the next tile's staging overwrites s_src
-  }
-}
-#endif
 
 // ------------------------------------------------------------------------------------
 // scans (u32 -> u64 exclusive), 3-phase reduce-then-scan

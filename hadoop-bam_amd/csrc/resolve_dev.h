@@ -29,9 +29,6 @@ namespace hbam {
 // 42.6 ms (profiles/r02/s2/ab_resolve_occupancy_10g.txt); 0 is not supported
 #define HBAM_RS_W 512
 #endif
-#ifndef HBAM_RS_NT_FAR
-#define HBAM_RS_NT_FAR 0  // A/B: far sources further back than this many bytes loaded non-temporal
-#endif
 #ifndef HBAM_RS_S
 #define HBAM_RS_S 1024  // A/B at 2 GB (window 1 KiB): 2048 -> 16.8 ms, 1024 -> 11.7 ms
 #endif
@@ -133,125 +130,6 @@ __device__ __forceinline__ uint32_t lds_rd32u(const uint8_t* buf, uint32_t x) {
   return __builtin_amdgcn_alignbit(*(const uint32_t*)(buf + a + 4u), *(const uint32_t*)(buf + a), (x & 3u) * 8u);
 }
 
-#ifdef HBAM_RS_ALIGNED
-// Every LDS access at its natural alignment (cdna_hip_programming.md Guideline 17: ds_read/write
-// _b64/_b128 off 8/16-byte alignment replay): bytes at any index are assembled from aligned
-// dwords with v_alignbit, and a destination that is not 4-aligned is written as b8/b16 pieces up
-// to the next dword.  LDS indices are u32 offsets from buf (16-byte aligned).
-__device__ __forceinline__ uint32_t lw(const uint8_t* buf, uint32_t a) {  // a % 4 == 0
-  return *(const uint32_t*)(buf + a);
-}
-__device__ __forceinline__ void lwr(uint8_t* buf, uint32_t a, uint32_t v) { *(uint32_t*)(buf + a) = v; }
-typedef uint32_t rs_u32a1 __attribute__((aligned(1)));
-typedef uint64_t rs_u64a1 __attribute__((aligned(1)));
-// 8 bytes at any index x
-__device__ __forceinline__ uint64_t lds_rd64u(const uint8_t* buf, uint32_t x) {
-  const uint32_t a = x & ~3u, sh = (x & 3u) * 8u;
-  const uint32_t w0 = lw(buf, a), w1 = lw(buf, a + 4u), w2 = lw(buf, a + 8u);
-  return (uint64_t)__builtin_amdgcn_alignbit(w1, w0, sh) | (uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh) << 32;
-}
-// bytes [x, x + n) (n <= 8) from the low bytes of v, every store naturally aligned
-__device__ __forceinline__ void lds_wr_small(uint8_t* buf, uint32_t x, uint64_t v, uint32_t n) {
-  if ((x & 1u) && n) { buf[x] = (uint8_t)v; v >>= 8; x += 1u; n -= 1u; }
-  if ((x & 2u) && n >= 2u) { *(uint16_t*)(buf + x) = (uint16_t)v; v >>= 16; x += 2u; n -= 2u; }
-  if (n >= 4u) { lwr(buf, x, (uint32_t)v); v >>= 32; x += 4u; n -= 4u; }
-  if (n >= 4u) { lwr(buf, x, (uint32_t)v); v >>= 32; x += 4u; n -= 4u; }
-  if (n >= 2u) { *(uint16_t*)(buf + x) = (uint16_t)v; v >>= 16; x += 2u; n -= 2u; }
-  if (n) buf[x] = (uint8_t)v;
-}
-// LZ77 copy inside the LDS window: dst index di, len bytes from di - dist (sources final).
-__device__ __forceinline__ void rs_copy_lds(uint8_t* __restrict__ buf, uint32_t di, uint32_t len,
-                                            uint32_t dist, const uint64_t* __restrict__ s_sel) {
-  if (dist < 8u) {
-    // period < 8: the bytes up to the first 4-aligned index >= di + 3 from the 8-byte pattern,
-    // then whole dwords from a register recurrence: dword [D, D + 4) = bytes [D - pd, D - pd + 4)
-    // with pd a multiple of dist >= 4 (so every byte it needs is before D and already final)
-    const uint64_t pat = periodic8(lds_rd64u(buf, di - dist), s_sel[dist]);
-    uint32_t h = ((di + 6u) & ~3u) - di;
-    if (h > len) h = len;
-    lds_wr_small(buf, di, pat, h);
-    if (h == len) return;
-    const uint32_t pd = (dist == 1u || dist == 2u) ? 4u : (dist == 3u) ? 6u : dist;
-    const uint32_t sh = (8u - pd) * 8u;  // pd = 4: the next dword is hi
-    uint32_t lo = lw(buf, di + h - 8u), hi = lw(buf, di + h - 4u);
-    uint32_t t = h;
-    for (; t + 4u <= len; t += 4u) {
-      const uint32_t nw = pd == 4u ? hi : __builtin_amdgcn_alignbit(hi, lo, sh);
-      lwr(buf, di + t, nw);
-      lo = hi;
-      hi = nw;
-    }
-    if (t < len) lds_wr_small(buf, di + t, pd == 4u ? hi : __builtin_amdgcn_alignbit(hi, lo, sh), len - t);
-    return;
-  }
-  // dist >= 8: the head up to 4-alignment, then 4-aligned dwords assembled from the source's
-  // aligned dwords (every source byte of a group lies before the group's destination)
-  uint32_t h = (0u - di) & 3u;
-  if (h > len) h = len;
-  if (h) lds_wr_small(buf, di, lds_rd32u(buf, di - dist), h);
-  const uint32_t sh = ((0u - dist) & 3u) * 8u;
-  uint32_t t = h;
-  if (dist >= 16u || dist >= len) {
-    for (; t < len; t += 16u) {  // 16-byte groups: 5 source dwords -> 4 destination dwords
-      const uint32_t a = (di + t - dist) & ~3u;
-      const uint32_t w0 = lw(buf, a), w1 = lw(buf, a + 4u), w2 = lw(buf, a + 8u), w3 = lw(buf, a + 12u),
-                     w4 = lw(buf, a + 16u);
-      const uint32_t o0 = __builtin_amdgcn_alignbit(w1, w0, sh), o1 = __builtin_amdgcn_alignbit(w2, w1, sh),
-                     o2 = __builtin_amdgcn_alignbit(w3, w2, sh), o3 = __builtin_amdgcn_alignbit(w4, w3, sh);
-      const uint32_t n = len - t;
-      if (n >= 16u) {
-        lwr(buf, di + t, o0);
-        lwr(buf, di + t + 4u, o1);
-        lwr(buf, di + t + 8u, o2);
-        lwr(buf, di + t + 12u, o3);
-      } else if (n >= 8u) {
-        lwr(buf, di + t, o0);
-        lwr(buf, di + t + 4u, o1);
-        lds_wr_small(buf, di + t + 8u, (uint64_t)o2 | (uint64_t)o3 << 32, n - 8u);
-      } else {
-        lds_wr_small(buf, di + t, (uint64_t)o0 | (uint64_t)o1 << 32, n);
-      }
-    }
-  } else {
-    for (; t < len; t += 8u) {  // 8 <= dist < 16, overlapping: 8-byte groups in order
-      const uint32_t a = (di + t - dist) & ~3u;
-      const uint32_t w0 = lw(buf, a), w1 = lw(buf, a + 4u), w2 = lw(buf, a + 8u);
-      const uint32_t o0 = __builtin_amdgcn_alignbit(w1, w0, sh), o1 = __builtin_amdgcn_alignbit(w2, w1, sh);
-      const uint32_t n = len - t;
-      if (n >= 8u) {
-        lwr(buf, di + t, o0);
-        lwr(buf, di + t + 4u, o1);
-      } else {
-        lds_wr_small(buf, di + t, (uint64_t)o0 | (uint64_t)o1 << 32, n);
-      }
-    }
-  }
-}
-// copy len bytes from final global bytes g (dist > len) into the LDS window at index di: global
-// loads at any alignment, LDS stores 4-aligned after a head of < 4 bytes
-__device__ __forceinline__ void rs_copy_glb(uint8_t* __restrict__ buf, uint32_t di, uint32_t len,
-                                            const uint8_t* __restrict__ g) {
-  uint32_t h = (0u - di) & 3u;
-  if (h > len) h = len;
-  if (h) lds_wr_small(buf, di, *(const rs_u32a1*)g, h);
-  for (uint32_t t = h; t < len; t += 16u) {
-    const uint64_t v0 = *(const rs_u64a1*)(g + t), v1 = *(const rs_u64a1*)(g + t + 8);
-    const uint32_t n = len - t;
-    if (n >= 16u) {
-      lwr(buf, di + t, (uint32_t)v0);
-      lwr(buf, di + t + 4u, (uint32_t)(v0 >> 32));
-      lwr(buf, di + t + 8u, (uint32_t)v1);
-      lwr(buf, di + t + 12u, (uint32_t)(v1 >> 32));
-    } else if (n >= 8u) {
-      lwr(buf, di + t, (uint32_t)v0);
-      lwr(buf, di + t + 4u, (uint32_t)(v0 >> 32));
-      lds_wr_small(buf, di + t + 8u, v1, n - 8u);
-    } else {
-      lds_wr_small(buf, di + t, v0, n);
-    }
-  }
-}
-#else
 // LZ77 copy inside the LDS window: dst index di, len bytes from di - dist (sources final).
 __device__ __forceinline__ void rs_copy_lds(uint8_t* __restrict__ buf, uint32_t di, uint32_t len,
                                             uint32_t dist, const uint64_t* __restrict__ s_sel) {
@@ -302,26 +180,7 @@ __device__ __forceinline__ void rs_copy_glb(uint8_t* __restrict__ buf, uint32_t 
     if (n > 24u) lds_wr_part(d + t + 24, v3, n - 24u);
   }
 }
-#endif
 
-#if HBAM_RS_NT_FAR
-// rs_copy_glb with non-temporal 8-byte loads
-__device__ __forceinline__ void rs_copy_glb_nt(uint8_t* __restrict__ buf, uint32_t di, uint32_t len,
-                                               const uint8_t* __restrict__ g) {
-  uint8_t* d = buf + di;
-  for (uint32_t t = 0; t < len; t += 32u) {
-    const uint64_t v0 = __builtin_nontemporal_load((const uint64_t*)(g + t)),
-                   v1 = __builtin_nontemporal_load((const uint64_t*)(g + t + 8)),
-                   v2 = __builtin_nontemporal_load((const uint64_t*)(g + t + 16)),
-                   v3 = __builtin_nontemporal_load((const uint64_t*)(g + t + 24));
-    const uint32_t n = len - t;
-    lds_wr_part(d + t, v0, n);
-    if (n > 8u) lds_wr_part(d + t + 8, v1, n - 8u);
-    if (n > 16u) lds_wr_part(d + t + 16, v2, n - 16u);
-    if (n > 24u) lds_wr_part(d + t + 24, v3, n - 24u);
-  }
-}
-#endif
 
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
 #pragma unroll
