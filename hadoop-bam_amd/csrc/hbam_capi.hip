@@ -2073,8 +2073,14 @@ extern "C" int hbam_gather_records(hbam_ctx* c, const uint8_t* ubuf, const uint6
   if (n) {
     // one wave per record, grid-stride: a grid of 64 x n threads would pass 2^32 above 67 M
     // records (the dispatch packet's grid size is 32-bit)
+#if HBAM_GATHER_TILE
+    // a wave per 64-record tile (A/B against the wave-per-record gather: profiles/r04/ab/)
+    k_gather_records_tile<<<(uint32_t)std::min<uint64_t>((n + 255) / 256, POOLS_MAX_WG), 256, 0, c->stream>>>(
+        ubuf, rec_off, perm, n, out_off, out);
+#else
     const uint64_t g = std::min<uint64_t>((n + RS_WG / 64 - 1) / (RS_WG / 64), GATHER_MAX_WG);
     k_gather_records<<<(uint32_t)g, RS_WG, 0, c->stream>>>(ubuf, rec_off, perm, n, out_off, out);
+#endif
   }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev[10], c->stream));

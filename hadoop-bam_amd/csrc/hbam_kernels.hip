@@ -916,25 +916,45 @@ static __device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t* p) {
   return (uint64_t)ld_u32_unaligned(p) | (uint64_t)ld_u32_unaligned(p + 4) << 32;
 }
 // MurmurHash3.murmurhash3(byte[], seed=0) incl. the h2 quirk of MurmurHash3.java:59
+// The 16-byte blocks are loaded MH_BATCH at a time, all loads of a batch in flight together,
+// and the tail as two 8-byte loads (masked): an unmapped read's hash (the whole variable part,
+// ~19 blocks) used to wait for one dependent load pair per block plus one per tail byte, and
+// with ~1 % unmapped reads about half of the waves carried one such lane.
+#ifndef HBAM_MH_BATCH
+#define HBAM_MH_BATCH 8
+#endif
 static __device__ uint64_t murmur3_java(const uint8_t* __restrict__ key, int32_t len) {
   const int32_t nblocks = len / 16;
   uint64_t h1 = 0, h2 = 0;
   const uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
-  for (int32_t i = 0; i < nblocks; ++i) {
-    uint64_t k1 = ld_u64_unaligned(key + 16 * i), k2 = ld_u64_unaligned(key + 16 * i + 8);
-    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
-    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
-    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
-    h2 = h2 << 31 | h1 >> 33;
-    h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+  for (int32_t i0 = 0; i0 < nblocks; i0 += HBAM_MH_BATCH) {
+    uint64_t kk[2 * HBAM_MH_BATCH];
+#pragma unroll
+    for (int32_t j = 0; j < HBAM_MH_BATCH; ++j) {
+      const uint8_t* q = key + 16 * (i0 + j < nblocks ? i0 + j : i0);  // past the last block: re-read one
+      kk[2 * j] = ld_u64_unaligned(q);
+      kk[2 * j + 1] = ld_u64_unaligned(q + 8);
+    }
+#pragma unroll
+    for (int32_t j = 0; j < HBAM_MH_BATCH; ++j) {
+      if (i0 + j < nblocks) {
+        uint64_t k1 = kk[2 * j], k2 = kk[2 * j + 1];
+        k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+        h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+        k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+        h2 = h2 << 31 | h1 >> 33;
+        h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+      }
+    }
   }
+  // tail: t < 16 bytes as little-endian words (over-reads stay inside ubuf + slack)
   const uint8_t* tail = key + 16 * nblocks;
   const int32_t t = len & 15;
-  uint64_t k1 = 0, k2 = 0;
-  for (int32_t i = t - 1; i >= 8; --i) k2 ^= (uint64_t)tail[i] << (8 * (i - 8));
-  if (t > 8) { k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2; }
-  for (int32_t i = (t < 8 ? t : 8) - 1; i >= 0; --i) k1 ^= (uint64_t)tail[i] << (8 * i);
-  if (t > 0) { k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1; }
+  const uint64_t w0 = ld_u64_unaligned(tail), w1 = ld_u64_unaligned(tail + 8);
+  const uint64_t k1 = t >= 8 ? w0 : (t > 0 ? w0 & ((1ull << (8 * t)) - 1ull) : 0ull);
+  const uint64_t k2 = t > 8 ? w1 & (t == 16 ? ~0ull : ((1ull << (8 * (t - 8))) - 1ull)) : 0ull;
+  if (t > 8) { uint64_t k = k2; k *= c2; k = rotl64(k, 33); k *= c1; h2 ^= k; }
+  if (t > 0) { uint64_t k = k1; k *= c1; k = rotl64(k, 31); k *= c2; h1 ^= k; }
   h1 ^= (uint64_t)(int64_t)len;
   h2 ^= (uint64_t)(int64_t)len;
   h1 += h2;

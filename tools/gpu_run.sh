@@ -13,7 +13,7 @@
 #   bin,PATH             run a probe executable (tools/probes/*)
 #   abdecode,SIZE,LIBS   tools/ab_decode.py A/B of library builds (LIBS separated by '+')
 #   stream,SIZE,WINDOW   tools/bench_stream.py (config #4 share)
-#   sort,SIZE            tools/bench_sort.py (config #5 share)
+#   sort,SIZE[,LIB]      tools/bench_sort.py (config #5 share), optionally against hadoop-bam_amd/LIB
 #   guess,SIZE           tools/bench_guess.py (config #3)
 #   crc                  tools/check_inflate_crc.py
 #   calib                rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/pmc_calib (known bytes per shape)
@@ -57,8 +57,10 @@ for spec in "$@"; do
       timeout -k 10 900 python -u tools/ab_decode.py --size ${a1:-5e9} --reps ${a3:-3} --libs ${a2//+/ } > $O/ab_${a2//+/_}.txt 2>&1; r=$? ;;
     stream)
       timeout -k 10 600 python -u tools/bench_stream.py --size ${a1:-25e9} --window ${a2:-2e9} --reps 2 > $O/stream.json 2> $O/stream.err; r=$? ;;
-    sort)
-      timeout -k 10 600 python -u tools/bench_sort.py --size ${a1:-12.5e9} > $O/sort.json 2> $O/sort.err; r=$? ;;
+    sort)  # sort[,SIZE[,LIB]]
+      if [ -n "$a2" ]; then export HBAM_LIB=hadoop-bam_amd/$a2; fi
+      timeout -k 10 600 python -u tools/bench_sort.py --size ${a1:-12.5e9} > $O/sort${a2:+_$a2}.json 2> $O/sort${a2:+_$a2}.err; r=$?
+      unset HBAM_LIB ;;
     guess)
       timeout -k 10 700 python -u tools/bench_guess.py --size ${a1:-50e9} --guesses 10000 --check 10000 > $O/guess.json 2> $O/guess.err; r=$? ;;
     calib)  # FETCH_SIZE / WRITE_SIZE per access shape (tools/pmc_calib.hip, tools/pmc_calib.py)
