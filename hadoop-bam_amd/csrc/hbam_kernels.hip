@@ -76,16 +76,20 @@ __global__ __launch_bounds__(256) void k_scan_chunks(const uint8_t* __restrict__
   // each thread tests 16 consecutive positions per step using a 32-byte window
   // (requesting the next step's window before testing this one: 1.56 -> 1.71 ms at 5 GB,
   // profiles/r03/ab/scan_prefetch_5g.txt; not kept)
-  for (uint32_t step = 0; step < SCAN_CHUNK / (256 * 16); ++step) {
-    const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * 16;
+#ifndef HBAM_SCAN_POS
+#define HBAM_SCAN_POS 32  // positions per thread per step: 16 -> 32 keeps twice the bytes in flight, 1.55 -> 1.40 ms at 5 GB (profiles/r04/ab/scan_32_positions_5g.txt)
+#endif
+  constexpr int SP = HBAM_SCAN_POS;
+  for (uint32_t step = 0; step < SCAN_CHUNK / (256 * SP); ++step) {
+    const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * SP;
     if (p0 >= end) break;
-    // 16-byte aligned relative to comp (begin is 16-aligned by construction of callers? no:
-    // use byte loads for the window to stay alignment-agnostic)
-    uint32_t w[9];
+    // byte-aligned dword loads (the compiler merges them into wide loads): positions p0..p0+SP-1
+    // need bytes up to p0 + SP + 11
+    uint32_t w[SP / 4 + 3];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
+    for (int i = 0; i < SP / 4 + 3; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < SP; ++k) {
       const uint64_t p = p0 + k;
       if (p + 18 > end) break;
       // bytes p..p+3 and p+10..p+11
