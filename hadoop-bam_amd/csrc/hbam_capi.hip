@@ -53,6 +53,7 @@ enum BufId {
   B_BITMAP,
   B_TAILS,
   B_EDGE,
+  B_RETRY,
   B_INFST,
   B_CRC,
   B_ENTRY,
@@ -489,6 +490,11 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   if ((rc = ensure(c, B_BITMAP, nb * BITMAP_WORDS, &bitmap))) return rc;
   if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
   if ((rc = ensure(c, B_EDGE, 32 * nb + 32, &edges))) return rc;
+  uint32_t* retry = nullptr;  // [HBAM_MAX_SLICES counters][nb block indices]
+#if HBAM_INFLATE_WAVE
+  if ((rc = ensure(c, B_RETRY, nb + HBAM_MAX_SLICES, &retry))) return rc;
+  if (nb) HIPCHK(c, hipMemsetAsync(retry, 0, HBAM_MAX_SLICES * 4, c->stream));
+#endif
   // Both passes are latency-bound at low occupancy (Huffman: 2 waves/SIMD; LZ77: a serial
   // walk per block), so the blocks are cut into slices and the LZ77 pass of slice s runs on a
   // second stream beside the Huffman pass of slice s+1: the CUs interleave the two kernels'
@@ -504,9 +510,19 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
       const uint64_t lo = nb * si / ns, hi = nb * (si + 1) / ns, n = hi - lo;
       if (!n) continue;
       hipStream_t rs = ns > 1 ? c->stream2 : c->stream;
+#if HBAM_INFLATE_WAVE
+      uint32_t* rl = retry + HBAM_MAX_SLICES + lo;
+      k_inflate_wave<<<(uint32_t)n, 64, 0, c->stream>>>(dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf,
+                                                       bitmap + lo * BITMAP_WORDS, tails + 2 * lo,
+                                                       edges + 32 * lo, st + lo, rl, retry + si);
       k_inflate_tokens<<<grid_for(n, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
           dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf, lens + lo * LENS_SLOT, bitmap + lo * BITMAP_WORDS,
-          tails + 2 * lo, edges + 32 * lo, st + lo);
+          tails + 2 * lo, edges + 32 * lo, st + lo, rl, retry + si);
+#else
+      k_inflate_tokens<<<grid_for(n, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
+          dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf, lens + lo * LENS_SLOT, bitmap + lo * BITMAP_WORDS,
+          tails + 2 * lo, edges + 32 * lo, st + lo, nullptr, nullptr);
+#endif
       if (ns > 1) {
         HIPCHK(c, hipEventRecord(c->slice_ev[si], c->stream));
         HIPCHK(c, hipStreamWaitEvent(rs, c->slice_ev[si], 0));
@@ -522,6 +538,26 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
     }
   }
   HIPCHK(c, hipGetLastError());
+#if HBAM_INFLATE_WAVE
+  if (nb && getenv("HBAM_WV_STATS")) {  // diagnostics: blocks the wave pass left to the lane pass
+    uint32_t cnt[HBAM_MAX_SLICES];
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(cnt, retry, sizeof(cnt), hipMemcpyDeviceToHost));
+    uint64_t tot = 0;
+    for (uint32_t si = 0; si < HBAM_MAX_SLICES; ++si) tot += cnt[si];
+    fprintf(stderr, "hbam: wave inflate left %llu of %llu blocks to the lane pass\n", (unsigned long long)tot,
+            (unsigned long long)nb);
+#ifdef HBAM_WV_PROF
+    unsigned long long pr[8];
+    HIPCHK(c, hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_wvprof), sizeof(pr)));
+    fprintf(stderr, "hbam: wave phases (Mcycles summed over waves): header %.1f tables %.1f count %.1f fix %.1f "
+            "offsets %.1f write %.1f; fix rounds %llu over %llu DEFLATE blocks\n", pr[0] / 1e6, pr[1] / 1e6,
+            pr[2] / 1e6, pr[3] / 1e6, pr[4] / 1e6, pr[5] / 1e6, pr[6], pr[7]);
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(g_wvprof), z, sizeof(z)));
+#endif
+  }
+#endif
   if (want_crc && nb) {
     k_crc32<<<grid_for(nb, 256), 256, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, crc);
     HIPCHK(c, hipGetLastError());

@@ -21,6 +21,7 @@
 #include "hbam_internal.h"
 #include "inflate_dev.h"
 #include "inflate_tok.h"
+#include "inflate_wave.h"
 #include "resolve_dev.h"
 
 namespace hbam {
@@ -243,11 +244,18 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
                                                                   uint32_t* __restrict__ bitmap,
                                                                   uint32_t* __restrict__ tails,
                                                                   uint8_t* __restrict__ edges,
-                                                                  int32_t* __restrict__ status) {
+                                                                  int32_t* __restrict__ status,
+                                                                  const uint32_t* __restrict__ list,
+                                                                  const uint32_t* __restrict__ nlist) {
   // 320 B of LDS per lane (u8 lit/len + distance symbols): 20 KiB per workgroup -> 8 per CU
   __shared__ uint8_t s_ll[INFLATE_WG * 288];
   __shared__ uint8_t s_d[INFLATE_WG * 32];
-  const uint32_t b = blockIdx.x * INFLATE_WG + threadIdx.x;
+  // list mode: the blocks k_inflate_wave left (list[0 .. *nlist)), else blocks 0 .. nblk
+  uint32_t b = blockIdx.x * INFLATE_WG + threadIdx.x;
+  if (list) {
+    if (b >= *nlist) return;
+    b = list[b];
+  }
   if (b >= nblk) return;
 #ifdef HBAM_PROF
   const uint64_t pr0 = PROF_RT(), pc0 = PROF_CLK();
@@ -295,6 +303,40 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
     g_prof[32 * (uint64_t)b + 11] = produced;
   }
 #endif
+}
+
+#ifndef HBAM_INFLATE_WAVE
+#define HBAM_INFLATE_WAVE 1  // Huffman pass: wave per block (inflate_wave.h) with the lane-per-block pass for the rest
+#endif
+// Huffman pass, one wave (= one workgroup) per BGZF block; see inflate_wave.h.  Blocks it does
+// not take are appended to list for k_inflate_tokens.
+__global__ __launch_bounds__(64, HBAM_WV_WAVES) void k_inflate_wave(const uint8_t* __restrict__ comp,
+                                                                   const BlockRec* __restrict__ blk,
+                                                                   const uint64_t* __restrict__ uoff,
+                                                                   uint32_t nblk, uint8_t* __restrict__ ubuf,
+                                                                   uint32_t* __restrict__ bitmap,
+                                                                   uint32_t* __restrict__ tails,
+                                                                   uint8_t* __restrict__ edges,
+                                                                   int32_t* __restrict__ status,
+                                                                   uint32_t* __restrict__ list,
+                                                                   uint32_t* __restrict__ nlist) {
+  __shared__ WvLds S;
+  const uint32_t b = blockIdx.x;
+  if (b >= nblk) return;
+  const BlockRec r = blk[b];
+  bool ok = false;
+  if (r.isize >= 64u && r.isize <= 65536u && r.clen >= 26u + 8u) {
+    ok = inflate_wave_block(S, comp + r.coff + 18, r.clen - 26u, r.isize, ubuf, uoff[b],
+                            bitmap + (uint64_t)b * BITMAP_WORDS, edges + 32 * (uint64_t)b);
+  }
+  if (threadIdx.x == 0) {
+    if (ok) {
+      tails[2 * (uint64_t)b] = 0;
+      status[b] = INF_OK;
+    } else {
+      list[atomicAdd(nlist, 1u)] = b;
+    }
+  }
 }
 
 // The partial first / last chunks of each block (TSink edge slots) -> this block's bytes of
