@@ -15,8 +15,9 @@ the barrier; scaling is weak (per-GPU bytes fixed).  Records of a BGZF block tha
 at a split boundary are read by both neighbouring splits, as in the reference; the record count
 check subtracts them.
 
-Prints ONE JSON line (rank 0).  roofline = the dominant kernel (k_inflate_tokens) with HIP
-events on the context's stream, plus per-stage and whole-pipeline fractions; cpu_baseline = the
+Prints ONE JSON line (rank 0).  roofline = the dominant kernel (the Huffman pass: k_inflate_tokens
+at this size, k_inflate_wave for calls of up to HBAM_WAVE_MAX_BLOCKS blocks) with HIP events on
+the context's stream, plus per-stage and whole-pipeline fractions; cpu_baseline = the
 oracle's C restatement on a bounded sample on the host cores; parity = random FileVirtualSplits
 of the benchmarked file re-read by the oracle outside the timed region.
 """
@@ -36,6 +37,9 @@ import numpy as np  # noqa: E402
 
 METRIC = "uncompressed BAM GB/s + records/s decoded (whole node, 1/2/4/8 MI355X)"
 HBM_PEAK_GBS = 8000.0
+# the library's Huffman pass: k_inflate_wave for calls of up to HBAM_WAVE_MAX_BLOCKS blocks
+# (hbam_capi.hip), k_inflate_tokens above (a 10 GB shard: ~390k blocks)
+WAVE_MAX_BLOCKS = int(os.environ.get("HBAM_WAVE_MAX_BLOCKS", "90000"))
 N_REF = 25  # the generator's dictionary (tools/gen_bam.cpp)
 
 
@@ -405,14 +409,17 @@ def main():
     achieved = alg / (inf_ms / 1e3) / 1e9
     traffic, traffic_src = None, None
     # the newest committed PMC pass of this kernel over the same workload (tools/pmc_summarize.py)
-    for rnd, tree in (("r04", "round4"), ("r03", "round3"), ("r02", "round2")):
-        pmc = os.path.join(ROOT, "profiles", rnd, "pmc_k_inflate_tokens.json")
+    huff_kernel = "k_inflate_wave" if nblk <= WAVE_MAX_BLOCKS else "k_inflate_tokens"
+    pmc_files = ((("r04", "round4-wave", "pmc_huffman.json"),) if huff_kernel == "k_inflate_wave" else
+                 (("r04", "round4", "pmc_k_inflate_tokens.json"), ("r03", "round3", "pmc_k_inflate_tokens.json")))
+    for rnd, tree, fname in pmc_files:
+        pmc = os.path.join(ROOT, "profiles", rnd, fname)
         if traffic is None and os.path.exists(pmc):
             try:
                 pj = json.load(open(pmc))
                 if pj.get("comp_bytes") and abs(pj["comp_bytes"] - C_b) / C_b < 0.05 and \
-                        pj.get("kernel") == "k_inflate_tokens" and pj.get("tree") == tree:
-                    traffic, traffic_src = pj.get("hbm_bytes_per_launch"), "profiles/%s/pmc_k_inflate_tokens.json" % rnd
+                        pj.get("kernel") == huff_kernel and pj.get("tree") == tree:
+                    traffic, traffic_src = pj.get("hbm_bytes_per_launch"), "profiles/%s/%s" % (rnd, fname)
             except Exception:
                 traffic = None
     result = {
@@ -431,7 +438,7 @@ def main():
         "stages_ms": {k: round(avg[k], 3) for k in ("scan_ms", "inflate_ms", "huffman_ms",
                                                     "resolve_ms", "walk_ms", "decode_ms",
                                                     "pools_ms", "total_ms")},
-        "roofline": {"bound": "hbm", "kernel": "k_inflate_tokens", "achieved": round(achieved, 2),
+        "roofline": {"bound": "hbm", "kernel": huff_kernel, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": int(alg),

@@ -185,6 +185,14 @@ enum BufId {
 #define HBAM_INFLATE_SLICES 1  // A/B at 10 GB: 1 -> 163.4 ms, 2 -> 161.5, 4 -> 166.5, 8 -> 164.5 (Huffman + LZ77)
 #endif
 #define HBAM_MAX_SLICES 16
+#ifndef HBAM_WAVE_MAX_BLOCKS
+// Huffman pass by k_inflate_wave (a wave per block) for calls of up to this many BGZF blocks,
+// by k_inflate_tokens (a lane per block) above: the lane pass needs ~131k blocks (2 waves x 64
+// lanes x 1,024 SIMDs) to fill the chip, the wave pass fills it from a few thousand but costs
+// more per block.  Huffman ms, lane vs wave: 1 GB 16.8 / 9.5, 2 GB 20.8 / 18.2, 3 GB 21.5 / 27.0,
+// 5 GB 33.8 / 44.7, 10 GB 60 / 88.9 (profiles/r04/ab/huffman_wave_vs_lane_by_size.txt)
+#define HBAM_WAVE_MAX_BLOCKS 90000
+#endif
 struct hbam_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -195,6 +203,7 @@ struct hbam_ctx {
   hipEvent_t ev[16];
   hipEvent_t slice_ev[HBAM_MAX_SLICES + 1];
   uint32_t inflate_slices = HBAM_INFLATE_SLICES;  // env HBAM_INFLATE_SLICES overrides (A/B)
+  uint64_t wave_max_blocks = HBAM_WAVE_MAX_BLOCKS;  // env HBAM_WAVE_MAX_BLOCKS overrides (tests, A/B)
   bool slices_forced = false;                     // ... and then applies to small calls too
   hbam_timing timing{};
   uint64_t* pinned_small = nullptr;  // host pinned scalars
@@ -491,10 +500,11 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
   if ((rc = ensure(c, B_EDGE, 32 * nb + 32, &edges))) return rc;
   uint32_t* retry = nullptr;  // [HBAM_MAX_SLICES counters][nb block indices]
-#if HBAM_INFLATE_WAVE
-  if ((rc = ensure(c, B_RETRY, nb + HBAM_MAX_SLICES, &retry))) return rc;
-  if (nb) HIPCHK(c, hipMemsetAsync(retry, 0, HBAM_MAX_SLICES * 4, c->stream));
-#endif
+  const bool wave = HBAM_INFLATE_WAVE && nb <= c->wave_max_blocks;
+  if (wave) {
+    if ((rc = ensure(c, B_RETRY, nb + HBAM_MAX_SLICES, &retry))) return rc;
+    HIPCHK(c, hipMemsetAsync(retry, 0, HBAM_MAX_SLICES * 4, c->stream));
+  }
   // Both passes are latency-bound at low occupancy (Huffman: 2 waves/SIMD; LZ77: a serial
   // walk per block), so the blocks are cut into slices and the LZ77 pass of slice s runs on a
   // second stream beside the Huffman pass of slice s+1: the CUs interleave the two kernels'
@@ -510,19 +520,19 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
       const uint64_t lo = nb * si / ns, hi = nb * (si + 1) / ns, n = hi - lo;
       if (!n) continue;
       hipStream_t rs = ns > 1 ? c->stream2 : c->stream;
-#if HBAM_INFLATE_WAVE
-      uint32_t* rl = retry + HBAM_MAX_SLICES + lo;
-      k_inflate_wave<<<(uint32_t)n, 64, 0, c->stream>>>(dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf,
-                                                       bitmap + lo * BITMAP_WORDS, tails + 2 * lo,
-                                                       edges + 32 * lo, st + lo, rl, retry + si);
-      k_inflate_tokens<<<grid_for(n, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
-          dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf, lens + lo * LENS_SLOT, bitmap + lo * BITMAP_WORDS,
-          tails + 2 * lo, edges + 32 * lo, st + lo, rl, retry + si);
-#else
-      k_inflate_tokens<<<grid_for(n, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
-          dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf, lens + lo * LENS_SLOT, bitmap + lo * BITMAP_WORDS,
-          tails + 2 * lo, edges + 32 * lo, st + lo, nullptr, nullptr);
-#endif
+      if (wave) {
+        uint32_t* rl = retry + HBAM_MAX_SLICES + lo;
+        k_inflate_wave<<<(uint32_t)n, 64, 0, c->stream>>>(dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf,
+                                                         bitmap + lo * BITMAP_WORDS, tails + 2 * lo,
+                                                         edges + 32 * lo, st + lo, rl, retry + si);
+        k_inflate_tokens<<<grid_for(n, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
+            dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf, lens + lo * LENS_SLOT, bitmap + lo * BITMAP_WORDS,
+            tails + 2 * lo, edges + 32 * lo, st + lo, rl, retry + si);
+      } else {
+        k_inflate_tokens<<<grid_for(n, INFLATE_WG), INFLATE_WG, 0, c->stream>>>(
+            dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf, lens + lo * LENS_SLOT, bitmap + lo * BITMAP_WORDS,
+            tails + 2 * lo, edges + 32 * lo, st + lo, nullptr, nullptr);
+      }
       if (ns > 1) {
         HIPCHK(c, hipEventRecord(c->slice_ev[si], c->stream));
         HIPCHK(c, hipStreamWaitEvent(rs, c->slice_ev[si], 0));
@@ -539,7 +549,7 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   }
   HIPCHK(c, hipGetLastError());
 #if HBAM_INFLATE_WAVE
-  if (nb && getenv("HBAM_WV_STATS")) {  // diagnostics: blocks the wave pass left to the lane pass
+  if (wave && nb && getenv("HBAM_WV_STATS")) {  // diagnostics: blocks the wave pass left to the lane pass
     uint32_t cnt[HBAM_MAX_SLICES];
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(cnt, retry, sizeof(cnt), hipMemcpyDeviceToHost));
@@ -597,6 +607,7 @@ hbam_ctx* hbam_create(int device_ordinal, const hbam_opts* opts) {
       c->slices_forced = true;
     }
   }
+  if (const char* wm = getenv("HBAM_WAVE_MAX_BLOCKS")) c->wave_max_blocks = strtoull(wm, nullptr, 10);
   if (const char* gb = getenv("HBAM_GUESS_BATCH")) {
     const long v = strtol(gb, nullptr, 10);
     if (v > 0) c->guess_batch = (uint64_t)v;

@@ -334,6 +334,16 @@ __device__ bool wv_header(WvLds& S, WvHdr& h, uint32_t& q, uint32_t E, bool& bfi
 // so that a token can be decoded speculatively and committed with selects: the decode loops
 // below have no divergent branches around the decode, which keeps the compiler from copying the
 // reader's registers (and waiting on the quad in flight) at every iteration.
+#ifndef HBAM_WV_NT
+#define HBAM_WV_NT 0  // non-temporal input quads (A/B)
+#endif
+__device__ __forceinline__ u32x4_t wv_load(const uint4* p) {
+#if HBAM_WV_NT
+  return __builtin_nontemporal_load((const u32x4_t*)p);
+#else
+  return ein_load(p);
+#endif
+}
 struct WvBits {
   uint64_t bb;
   uint32_t bc, rd, nv, pos;  // valid bits, next bank dword, dwords left in the banks, word-bit position
@@ -365,7 +375,7 @@ __device__ __forceinline__ void wv_in_at(WvIn& in, const uint32_t* cw, uint32_t 
   in.q0 = base[0];
   in.q1 = base[1];
   in.fp = base + 2 < in.fend ? base + 2 : in.fend;
-  in.t = ein_load(in.fp < in.fend ? in.fp : in.safe);
+  in.t = wv_load(in.fp < in.fend ? in.fp : in.safe);
   const uint32_t r = (uint32_t)(a >> 2), sh = 8u * (uint32_t)(a & 3u) + (p & 7u);
   in.s.bb = (uint64_t)(wv_sel(in, r) >> sh);
   in.s.bc = 32u - sh;
@@ -388,7 +398,7 @@ __device__ __forceinline__ void wv_epoch(WvIn& in) {
     in.s.nv += 4u;
     ++in.fp;
   }
-  in.t = ein_load(in.fp < in.fend ? in.fp : in.safe);
+  in.t = wv_load(in.fp < in.fend ? in.fp : in.safe);
 }
 __device__ __forceinline__ bool wv_short(const WvIn& in, uint32_t need) {
   return in.s.bc + 32u * in.s.nv < need && in.fp < in.fend;

@@ -232,6 +232,44 @@ def test_inflate_corrupted_blocks_match_zlib_classes(gpu_ctx, oracle_mod):
     assert len(set(int(x) for x in st)) >= 2  # the corruption exercised error paths
 
 
+@pytest.mark.parametrize("kw", [dict(seed=31), dict(seed=32, level=1), dict(seed=33, level=9),
+                                dict(seed=34, uniform_qual=1, level=6), dict(seed=35, level=0),
+                                dict(seed=36, payload=64, level=6)])
+def test_huffman_wave_and_lane_passes_agree(oracle_mod, genbam, monkeypatch, kw):
+    """The two Huffman passes (k_inflate_wave: a wave per block, used for calls of up to
+    HBAM_WAVE_MAX_BLOCKS blocks; k_inflate_tokens: a lane per block, above) give the same bytes
+    and statuses as zlib on the same blocks, corrupted ones included."""
+    from hadoop_bam import _lib
+    data = np.asarray(genbam.generate(records=6000, seed=kw["seed"],
+                                      **{k: v for k, v in kw.items() if k != "seed"})).copy()
+    ref = oracle_mod.scan_blocks(data)
+    bad = data.copy()
+    rng = np.random.default_rng(kw["seed"])
+    for i in range(0, len(ref["coff"]), 3):  # every third block: a bit flip
+        c, l = int(ref["coff"][i]), int(ref["clen"][i])
+        if l > 40:
+            p = c + 18 + int(rng.integers(0, l - 26))
+            bad[p] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    got = {}
+    for mode, limit in (("wave", "1000000000"), ("lane", "0")):
+        monkeypatch.setenv("HBAM_WAVE_MAX_BLOCKS", limit)
+        ctx = _lib.Context(0)
+        try:
+            got[mode] = [ctx.inflate(d, ref, check_crc=True) for d in (data, bad)]
+        finally:
+            ctx.close()
+    for (rw, uw, ow, sw), (rl, ul, ol, sl) in zip(got["wave"], got["lane"]):
+        assert rw == rl == 0
+        assert np.array_equal(sw, sl)
+        for i in range(len(ref["coff"])):
+            if int(sw[i]) == 0:
+                assert uw[int(ow[i]):int(ow[i + 1])].tobytes() == ul[int(ol[i]):int(ol[i + 1])].tobytes(), i
+    rc, u, off, st = got["wave"][0]
+    want = b"".join(zlib.decompressobj(-15).decompress(bytes(data[int(c) + 18:int(c) + int(l) - 8]))
+                    for c, l in zip(ref["coff"], ref["clen"]))
+    assert np.all(st == 0) and u.tobytes() == want
+
+
 @pytest.mark.parametrize("slices", [2, 3, 7])
 def test_sliced_inflate_pipeline(oracle_mod, monkeypatch, slices):
     """The Huffman / LZ77 passes cut into slices on two streams (HBAM_INFLATE_SLICES forces it

@@ -18,7 +18,8 @@ own access shapes by tools/pmc_calib.hip -> profiles/r04/calib/):
 
 usage: pmc_summarize.py FETCH_CSV WRITE_CSV COMP_BYTES OUT_DIR TREE [STAGES_JSON]
   STAGES_JSON: a bench.py line (its stages_ms give each kernel's unprofiled time)
-writes OUT_DIR/pmc_kernels.json (every kernel) and OUT_DIR/pmc_k_inflate_tokens.json (bench.py)
+writes OUT_DIR/pmc_kernels.json (every kernel) and OUT_DIR/pmc_huffman.json (bench.py: the Huffman
+pass, k_inflate_wave plus the lane-per-block k_inflate_tokens for the blocks it leaves)
 """
 import csv
 import json
@@ -26,7 +27,7 @@ import os
 import sys
 
 HBM_ACHIEVABLE = 6.3e12
-STAGE_OF = {"k_inflate_tokens": "huffman_ms", "k_resolve": "resolve_ms", "k_decode_pools": "pools_ms",
+STAGE_OF = {"k_inflate_wave": "huffman_ms", "k_inflate_tokens": "huffman_ms", "k_resolve": "resolve_ms", "k_decode_pools": "pools_ms",
             "k_decode_fixed": "decode_ms", "k_scan_chunks": "scan_ms"}
 
 
@@ -73,11 +74,19 @@ def main():
     json.dump({"tree": tree, "comp_bytes": int(comp), "note": note, "kernels": res},
               open(os.path.join(outdir, "pmc_kernels.json"), "w"), indent=1)
     h = res.get("k_inflate_tokens")
-    if h:
+    if h and "k_inflate_wave" not in res:  # a call above HBAM_WAVE_MAX_BLOCKS: the lane pass alone
         one = {"kernel": "k_inflate_tokens", "tree": tree, "comp_bytes": int(comp),
                "fetch_bytes_per_launch": h["fetch_bytes"], "write_bytes_per_launch": h["write_bytes"],
                "hbm_bytes_per_launch": h["hbm_bytes_per_launch"], "note": note}
         json.dump(one, open(os.path.join(outdir, "pmc_k_inflate_tokens.json"), "w"), indent=1)
+    h = res.get("k_inflate_wave")
+    if h:
+        lane = res.get("k_inflate_tokens", {"fetch_bytes": 0.0, "write_bytes": 0.0})
+        fb, wb = h["fetch_bytes"] + lane["fetch_bytes"], h["write_bytes"] + lane["write_bytes"]
+        one = {"kernel": "k_inflate_wave", "tree": tree, "comp_bytes": int(comp),
+               "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb,
+               "note": note + "; k_inflate_wave + the k_inflate_tokens launch over the blocks it leaves"}
+        json.dump(one, open(os.path.join(outdir, "pmc_huffman.json"), "w"), indent=1)
     for k, e in res.items():
         print("%-24s fetch %8.2f GB write %8.2f GB%s" % (k, e["fetch_bytes"] / 1e9, e["write_bytes"] / 1e9,
               ("  %.2f TB/s implied" % e["implied_tb_s"]) if "implied_tb_s" in e else ""))
