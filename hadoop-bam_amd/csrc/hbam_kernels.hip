@@ -221,6 +221,8 @@ __global__ void k_verify_chain(const uint8_t* __restrict__ comp, const uint64_t*
 
 // ------------------------------------------------------------------------------------
 // K2: inflate = two kernels.
+//  k_inflate_wave (phase 1, calls of up to HBAM_WAVE_MAX_BLOCKS blocks): one wave per BGZF
+//    block, same output; see inflate_wave.h.  Blocks it does not take go to k_inflate_tokens.
 //  k_inflate_tokens (phase 1): one lane per BGZF block (SIMT across blocks); Huffman
 //    decode with wave-uniform input epochs; literals land in ubuf, each match leaves a
 //    3-byte descriptor in its hole and a bit in the block's match-start bitmap (TSink,

@@ -330,10 +330,10 @@ __device__ bool wv_header(WvLds& S, WvHdr& h, uint32_t& q, uint32_t E, bool& bfi
 }
 
 // ---- lane reader: the input epochs of inflate_tok.h's EIn (two 16-byte banks + one quad in
-// flight, merged / requested by every lane at the same iteration), with the bit state kept apart
-// so that a token can be decoded speculatively and committed with selects: the decode loops
-// below have no divergent branches around the decode, which keeps the compiler from copying the
-// reader's registers (and waiting on the quad in flight) at every iteration.
+// flight, merged / requested by every lane at the same iteration); the decode loops are per-lane
+// do-while loops with a scalar epoch branch, as the lane pass's symbol loop (a wave-uniform
+// `while (__any(...))` loop made the compiler copy the reader's registers, and wait on the quad in
+// flight, at every iteration).
 #ifndef HBAM_WV_NT
 #define HBAM_WV_NT 0  // non-temporal input quads (A/B)
 #endif
@@ -417,13 +417,6 @@ __device__ __forceinline__ void wv_drop(WvBits& s, uint32_t n) {
   s.pos += n;
 }
 __device__ __forceinline__ uint32_t wv_peek(const WvBits& s, uint32_t n) { return (uint32_t)s.bb & ((1u << n) - 1u); }
-__device__ __forceinline__ void wv_commit(WvIn& in, const WvBits& s, bool c) {
-  in.s.bb = c ? s.bb : in.s.bb;
-  in.s.bc = c ? s.bc : in.s.bc;
-  in.s.rd = c ? s.rd : in.s.rd;
-  in.s.nv = c ? s.nv : in.s.nv;
-  in.s.pos = c ? s.pos : in.s.pos;
-}
 
 // One iteration of a decode loop: token A at s.pos, and when A is a literal whose successor
 // starts before `lim`, token B too (60 % of tokens are literals: 1.6 tokens per iteration, as
