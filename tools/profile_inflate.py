@@ -22,6 +22,7 @@ a = ap.parse_args()
 if a.prof:
     os.environ["HBAM_LIB"] = os.path.join(ROOT, "hadoop-bam_amd", "libhbam_prof.so")
     os.environ["HBAM_INFLATE_SLICES"] = "1"  # per-block prof slots are indexed per launch
+    os.environ["HBAM_WAVE_MAX_BLOCKS"] = "0"  # the stamps are in the lane-per-block Huffman pass
 g = genbam.generate(target_bytes=int(a.size), seed=a.seed, threads=16)
 data = np.asarray(g)
 d = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
