@@ -264,6 +264,17 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity-splits", type=int, default=32)
+    ap.add_argument("--sort-size", type=float, default=2e9,
+                    help="N > 1: compressed bytes per GPU of the unsorted file of the Sort leg (config #5 "
+                         "shape; 12.5e9 = config #5's per-GPU share at 8 GPUs)")
+    ap.add_argument("--sort-steps", type=int, default=2)
+    ap.add_argument("--no-sort", action="store_true", help="N > 1: skip the Sort leg")
+    ap.add_argument("--config4", action="store_true",
+                    help="BASELINE config #4 instead of the headline: ONE --c4-total file sharded over the N "
+                         "GPUs (strong scaling), each rank's share resident, decoded in windows (tools/config4.py)")
+    ap.add_argument("--c4-total", type=float, default=200e9, help="config #4 file size (compressed bytes)")
+    ap.add_argument("--c4-body", type=float, default=5e9, help="config #4: generated body repeated to fill the file")
+    ap.add_argument("--c4-window", type=float, default=0, help="config #4: window bytes (0: from free HBM)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -294,6 +305,20 @@ def main():
 
     from hadoop_bam import _lib
     ctx = _lib.Context(local)
+    if args.config4:
+        import config4
+        res = config4.run(ctx, dist, rank, world, args, dev, cdev, threads, N_REF, log, METRIC, parity_at_size)
+        if rank == 0:
+            body = res.pop("_body")
+            if not args.no_cpu_baseline:
+                try:
+                    res["cpu_baseline"] = cpu_baseline(body, args.cpu_budget, threads)
+                except Exception as e:  # baseline is reported, never the target
+                    res["cpu_baseline"] = {"error": str(e)}
+            print(json.dumps(res), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
 
     buf, own_len, off, file_len, n_own = make_shard(int(args.size), args.seed, rank, world,
                                                     threads, dist, cdev)
@@ -345,6 +370,7 @@ def main():
         k = min(n_rec, 4096)
         perm = torch.arange(k, dtype=torch.int32, device=dev)
         head = torch.empty(k, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()  # libhbam runs on its own stream: torch's arange must have landed
         assert ctx.L.hbam_permute(ctx.h, C.cast(cols.voffset, C.c_void_p), 8,
                                   C.c_void_p(perm.data_ptr()), k, C.c_void_p(head.data_ptr())) == 0
         overlap = int(((head.cpu() >> 16) == off).sum())
@@ -379,6 +405,15 @@ def main():
             del whole
         except Exception as e:  # reported, never hidden
             parity = {"error": str(e)}
+    sort_leg = None
+    if dist and not args.no_sort:
+        # config #5's leg across the ranks (cli/plugins/Sort.java:131-170), after the headline's timed
+        # region: decode + device sort + split points + exchange by key range (hbam_sort_exchange
+        # over RCCL on nccl), with its own parity (tools/sort_leg.py)
+        import sort_leg as sl
+        del cols
+        sort_leg = sl.run(ctx, dist, rank, world, int(args.sort_size), args.seed + 101, threads, dev, cdev,
+                          N_REF, steps=args.sort_steps, log=log)
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -449,6 +484,8 @@ def main():
                                   "what": "C + 2U + columns/pools over the whole decode"}},
         "parity": parity,
     }
+    if sort_leg is not None:
+        result["sort"] = sort_leg
     if not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(buf, args.cpu_budget, threads)

@@ -176,6 +176,7 @@ enum BufId {
   B_G_OOFF,
   B_G_BS,
   B_G_PAY,
+  B_RH_RECOFF,  // hbam_records_to_host: rec_off rebased to the copied record bytes
   B_COUNT_ALL
 };
 
@@ -208,6 +209,9 @@ struct hbam_ctx {
   hbam_timing timing{};
   uint64_t* pinned_small = nullptr;  // host pinned scalars
   uint64_t guess_batch = HBAM_GUESS_BATCH;  // env HBAM_GUESS_BATCH overrides (tests: multi-batch)
+  uint8_t* rec_host = nullptr;  // hbam_records_to_host: pinned, grow-only
+  size_t rec_host_cap = 0;
+  std::vector<hbam_comm*> comms;  // communicators tied to this context (hbam_comm.hip)
 };
 
 namespace {
@@ -619,16 +623,20 @@ hbam_ctx* hbam_create(int device_ordinal, const hbam_opts* opts) {
   return c;
 }
 
+void comm_detach(hbam_comm* m);  // hbam_comm.hip
 void hbam_destroy(hbam_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  // a communicator that outlives its context keeps its device ordinal only (hbam_comm_destroy)
+  for (hbam_comm* m : c->comms) comm_detach(m);
   for (auto& b : c->bufs)
     if (b.p) (void)hipFree(b.p);
   (void)hipStreamSynchronize(c->stream2);
   for (auto& e : c->ev) (void)hipEventDestroy(e);
   for (auto& e : c->slice_ev) (void)hipEventDestroy(e);
   if (c->pinned_small) (void)hipHostFree(c->pinned_small);
+  if (c->rec_host) (void)hipHostFree(c->rec_host);
   (void)hipStreamDestroy(c->stream2);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1633,6 +1641,74 @@ extern "C" void hbam_free_host_columns(hbam_columns* h) {
                 h->seq, h->qual, h->aux, h->ubuf};
   for (void* p : ps) free(p);
   memset(h, 0, sizeof *h);
+}
+
+namespace {
+__global__ void k_rebase_off(const uint64_t* __restrict__ in, uint64_t n, uint64_t lo, uint64_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = in[i] - lo;
+}
+}  // namespace
+
+// Records-only host copy for the drop-in reader (BAMRecordReader.nextKeyValue, :172-188, needs a
+// record's bytes, its key and its file pointer): 28 B of columns per record + the records' bytes,
+// into the context's pinned staging (one D2H pass at the DMA rate, no malloc per window).
+extern "C" int hbam_records_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_columns* h) {
+  if (!c || !dv || !h) return HBAM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  memset(h, 0, sizeof *h);
+  const uint64_t n = dv->n_records;
+  h->n_records = n;
+  h->status = dv->status;
+  h->err_record = dv->err_record;
+  if (!n) return HBAM_OK;
+  if (!dv->voffset || !dv->key || !dv->rec_off || !dv->block_size || !dv->ubuf) return HBAM_EINVAL;
+  // the records' byte range: first record's offset .. last record's end
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small, dv->rec_off, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small + 1, dv->rec_off + (n - 1), 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small + 2, dv->block_size + (n - 1), 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t lo = c->pinned_small[0];
+  const uint64_t hi = c->pinned_small[1] + 4 + (uint64_t)(uint32_t)c->pinned_small[2];
+  if (hi < lo || hi > dv->ubuf_len + UBUF_SLACK)
+    return set_err(c, HBAM_EINVAL, "hbam_records_to_host: record bytes outside ubuf");
+  const size_t cols = 8 * n * 3 + ((4 * n + 7) & ~(size_t)7);
+  const size_t need = cols + (hi - lo) + 64;
+  if (c->rec_host_cap < need) {
+    if (c->rec_host) (void)hipHostFree(c->rec_host);
+    c->rec_host = nullptr;
+    c->rec_host_cap = 0;
+    const size_t want = std::max(need, need + need / 4);
+    if (hipHostMalloc((void**)&c->rec_host, want, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      c->rec_host = nullptr;
+      return set_err(c, HBAM_ENOMEM, "hbam_records_to_host: hipHostMalloc(%zu) failed", want);
+    }
+    c->rec_host_cap = want;
+  }
+  uint64_t* roff;
+  int rc;
+  if ((rc = ensure(c, B_RH_RECOFF, n, &roff))) return rc;
+  k_rebase_off<<<(uint32_t)std::min<uint64_t>(grid_for(n, 256), 16384), 256, 0, c->stream>>>(dv->rec_off, n, lo, roff);
+  HIPCHK(c, hipGetLastError());
+  uint8_t* p = c->rec_host;
+  h->voffset = (uint64_t*)p;
+  h->key = (int64_t*)(p + 8 * n);
+  h->rec_off = (uint64_t*)(p + 16 * n);
+  h->block_size = (int32_t*)(p + 24 * n);
+  h->ubuf = p + cols;
+  h->ubuf_len = hi - lo;
+  HIPCHK(c, hipMemcpyAsync(h->voffset, dv->voffset, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(h->key, dv->key, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(h->rec_off, roff, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(h->block_size, dv->block_size, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(h->ubuf, dv->ubuf + lo, hi - lo, hipMemcpyDeviceToHost, c->stream));
+  const hipError_t e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    memset(h, 0, sizeof *h);
+    return set_err(c, HBAM_EDEVICE, "hbam_records_to_host: %s", hipGetErrorString(e));
+  }
+  return HBAM_OK;
 }
 
 extern "C" void hbam_release_columns(hbam_ctx* c, hbam_columns* dv) {

@@ -72,7 +72,8 @@ RcclApi& rccl() {
 }  // namespace
 
 struct hbam_comm {
-  hbam_ctx* c = nullptr;
+  hbam_ctx* c = nullptr;  // nullptr once the context is destroyed first (comm_detach)
+  int device = 0;
   ncclComm_t comm = nullptr;
   int32_t nranks = 0, rank = 0;
   // plan of the last size query (hbam_sort_exchange with out->payload == NULL)
@@ -100,7 +101,27 @@ int comm_check(hbam_ctx* c, hbam_comm* m) {
   return HBAM_OK;
 }
 
+// Every ncclGroupStart is matched by one ncclGroupEnd, on the error paths too: a group left
+// open would turn this thread's next RCCL call into part of it and hang the peers.
+struct GroupGuard {
+  bool open = false;
+  ncclResult_t start() {
+    const ncclResult_t r = rccl().GroupStart();
+    open = r == ncclSuccess;
+    return r;
+  }
+  ncclResult_t end() {
+    open = false;
+    return rccl().GroupEnd();
+  }
+  ~GroupGuard() {
+    if (open) (void)rccl().GroupEnd();
+  }
+};
+
 }  // namespace
+
+void comm_detach(hbam_comm* m) { m->c = nullptr; }
 
 extern "C" int hbam_comm_unique_id(uint8_t* id_out) {
   if (!id_out) return HBAM_EINVAL;
@@ -123,6 +144,7 @@ extern "C" int hbam_comm_init(hbam_ctx* c, const uint8_t* id, int32_t nranks, in
   memcpy(&uid, id, sizeof uid);
   hbam_comm* m = new hbam_comm();
   m->c = c;
+  m->device = c->device;
   m->nranks = nranks;
   m->rank = rank;
   const ncclResult_t r = R.CommInitRank(&m->comm, nranks, uid, rank);
@@ -130,17 +152,22 @@ extern "C" int hbam_comm_init(hbam_ctx* c, const uint8_t* id, int32_t nranks, in
     delete m;
     return set_err(c, HBAM_EDEVICE, "ncclCommInitRank(%d, %d): %s", nranks, rank, R.GetErrorString(r));
   }
+  c->comms.push_back(m);
   *out = m;
   return HBAM_OK;
 }
 
+// Either order of destruction is safe: with the context still alive its stream is drained and the
+// communicator unregistered; after hbam_destroy (which drained that stream) only the device is used.
 extern "C" void hbam_comm_destroy(hbam_comm* m) {
   if (!m) return;
-  if (m->comm) {
-    (void)hipSetDevice(m->c->device);
+  (void)hipSetDevice(m->device);
+  if (m->c) {
     (void)hipStreamSynchronize(m->c->stream);
-    (void)rccl().CommDestroy(m->comm);
+    auto& v = m->c->comms;
+    v.erase(std::remove(v.begin(), v.end(), m), v.end());
   }
+  if (m->comm) (void)rccl().CommDestroy(m->comm);
   delete m;
 }
 
@@ -234,7 +261,8 @@ extern "C" int hbam_sort_exchange(hbam_ctx* c, hbam_comm* m, const hbam_sorted_r
       (rc = ensure(c, B_X_BS, nr + 1, &rs)) || (rc = ensure(c, B_X_PAY, nb + 1, &rp)))
     return rc;
   HIPCHK(c, hipEventRecord(c->ev[12], c->stream));
-  NCCLCHK(c, R.GroupStart());
+  GroupGuard group;
+  NCCLCHK(c, group.start());
   for (uint32_t p = 0; p < P; ++p) {
     const uint64_t sr = m->rec_b[p + 1] - m->rec_b[p], sb = m->byte_b[p + 1] - m->byte_b[p];
     const uint64_t rr = roff[p + 1] - roff[p], rbb = rboff[p + 1] - rboff[p];
@@ -252,7 +280,7 @@ extern "C" int hbam_sort_exchange(hbam_ctx* c, hbam_comm* m, const hbam_sorted_r
       NCCLCHK(c, R.Recv(rp + rboff[p], rbb, ncclUint8, (int)p, m->comm, c->stream));
     }
   }
-  NCCLCHK(c, R.GroupEnd());
+  NCCLCHK(c, group.end());
   HIPCHK(c, hipEventRecord(c->ev[13], c->stream));
   if ((rc = hbam_sort_received(c, rk, rv, rs, rp, nr, out))) return rc;
   c->timing.exchange_ms = ev_ms(c, 12, 13);  // (hbam_sort_received reset the rest)

@@ -60,7 +60,7 @@ EXPORTS = [
     "hbam_host_register", "hbam_host_unregister", "hbam_bcf_parse_header", "hbam_guess_bcf_window_len",
     "hbam_guess_bcf_windows", "hbam_bcf_decode_split", "hbam_comm_unique_id", "hbam_comm_init",
     "hbam_comm_destroy", "hbam_comm_split_points", "hbam_sort_exchange", "hbam_split_open_reader",
-    "hbam_split_read_bytes", "hbam_rewrite_groups",
+    "hbam_split_read_bytes", "hbam_rewrite_groups", "hbam_records_to_host",
 ]
 
 # hbam_read_fn: int64_t read(void* user, uint64_t offset, uint64_t len, uint8_t* dst)
@@ -190,6 +190,7 @@ def load(path=None):
                                         C.c_uint64, C.c_uint64, C.c_int32, C.POINTER(Columns)]),
         "hbam_columns_to_host": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(Columns)]),
         "hbam_free_host_columns": (None, [C.POINTER(Columns)]),
+        "hbam_records_to_host": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(Columns)]),
         "hbam_release_columns": (None, [vp, C.POINTER(Columns)]),
         "hbam_guess_bam_record_start": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_int64,
                                                     C.c_int64, C.c_int32, _i32p]),
@@ -434,7 +435,8 @@ class Context:
         """Streamed BAMRecordReader over a host-resident file (hbam_split_open/next): yields
         the host columns of each window in order; the last one carries the split's status.
         host=False yields each window's device Columns struct instead (valid until the next
-        window is requested)."""
+        window is requested); host="records" the records-only copy (records_to_host: views, valid
+        until the next window is requested)."""
         a = np.ascontiguousarray(np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray)
                                  else data, dtype=np.uint8)
         keep = a if a.size else np.zeros(1, np.uint8)
@@ -452,6 +454,8 @@ class Context:
             b = read(int(off), int(n))
             if not b:
                 return -1
+            if len(b) > n:  # never past the n bytes of staging the library asked to fill
+                b = b[:n]
             C.memmove(dst, bytes(b), len(b))
             return len(b)
         fn = READ_FN(cb)
@@ -473,6 +477,9 @@ class Context:
                 if not host:
                     yield d
                     continue
+                if host == "records":
+                    yield self.records_to_host(d)
+                    continue
                 h = Columns()
                 rc = self.L.hbam_columns_to_host(self.h, C.byref(d), C.byref(h))
                 if rc:
@@ -484,6 +491,25 @@ class Context:
             self.last_stream_stats = self._split_stats(s)
             self.L.hbam_split_close(s)
             del keep
+
+    def records_to_host(self, d):
+        """hbam_records_to_host: what the drop-in reader hands out (key, voffset, rec_off, block_size
+        and the records' bytes), as numpy VIEWS of the context's pinned staging — valid until the
+        next call on this context.  d2h_bytes = what crossed PCIe."""
+        h = Columns()
+        rc = self.L.hbam_records_to_host(self.h, C.byref(d), C.byref(h))
+        if rc:
+            raise RuntimeError("hbam_records_to_host failed (%d): %s" % (rc, self.last_error()))
+        n = int(h.n_records)
+        out = {"n": n, "status": int(h.status), "err_record": int(h.err_record)}
+        for name, dt in (("voffset", np.uint64), ("key", np.int64), ("rec_off", np.uint64),
+                         ("block_size", np.int32)):
+            p = getattr(h, name)
+            out[name] = np.ctypeslib.as_array(p, shape=(n,)).view(dt) if n else np.zeros(0, dt)
+        ul = int(h.ubuf_len)
+        out["ubuf"] = np.ctypeslib.as_array(h.ubuf, shape=(ul,)) if (ul and h.ubuf) else np.zeros(0, np.uint8)
+        out["d2h_bytes"] = 28 * n + ul
+        return out
 
     def _split_stats(self, s):
         b, w = C.c_uint64(0), C.c_uint64(0)

@@ -490,79 +490,6 @@ class BGZFSplitFileInputFormat:
 
 
 # ---- record value -------------------------------------------------------------------
-class BAMRecordView:
-    """A lazily decoded BAM record (the SAMRecord the reader hands out): fixed fields
-    from the device columns, payload = the record's bytes in the inflated stream."""
-
-    __slots__ = ("_dec", "_i")
-
-    def __init__(self, dec, i):
-        self._dec, self._i = dec, i
-
-    def _c(self, k):
-        return self._dec.cols[k][self._i]
-
-    def getReferenceIndex(self):
-        return int(self._c("ref_id"))
-
-    def getAlignmentStart(self):
-        return int(np.int32(self._c("pos")) + np.int32(1))
-
-    def getFlags(self):
-        return int(self._c("flag"))
-
-    def getReadUnmappedFlag(self):
-        return bool(self.getFlags() & 4)
-
-    def getMappingQuality(self):
-        return int(self._c("mapq"))
-
-    def getMateReferenceIndex(self):
-        return int(self._c("next_ref_id"))
-
-    def getMateAlignmentStart(self):
-        return int(np.int32(self._c("next_pos")) + np.int32(1))
-
-    def getInferredInsertSize(self):
-        return int(self._c("tlen"))
-
-    def getIndexingBin(self):
-        return int(self._c("bin"))
-
-    def getReadName(self):
-        c = self._dec.cols
-        a, b = int(c["name_off"][self._i]), int(c["name_off"][self._i + 1])
-        return bytes(c["names"][a:max(a, b - 1)]).decode("latin-1")
-
-    def getCigarString(self):
-        c = self._dec.cols
-        a, b = int(c["cigar_off"][self._i]), int(c["cigar_off"][self._i + 1])
-        ops = c["cigars"][a:b]
-        if len(ops) == 0:
-            return "*"
-        return "".join("%d%s" % (int(v) >> 4, "MIDNSHP=X"[int(v) & 15]) for v in ops)
-
-    def getReadString(self):
-        c = self._dec.cols
-        a, b = int(c["seq_off"][self._i]), int(c["seq_off"][self._i + 1])
-        return bytes(c["seq"][a:b]).decode() or "*"
-
-    def getBaseQualities(self):
-        c = self._dec.cols
-        a, b = int(c["seq_off"][self._i]), int(c["seq_off"][self._i + 1])
-        return bytes(c["qual"][a:b])
-
-    def getReadBases(self):
-        return self.getReadString().encode() if self.getReadString() != "*" else b""
-
-    def getVariableBinaryRepresentation(self):
-        return self._dec.var_block(self._i)
-
-    def toBAMBytes(self):
-        """block_size + the record (what BAMRecordCodec.encode writes for an untouched record)."""
-        return self._dec.record_bytes(self._i)
-
-
 class SAMRecordWritable:
     """SAMRecordWritable.java:46-70."""
 
@@ -770,7 +697,8 @@ def _i32(x):
 
 
 class _DecodedSplit:
-    """One window's host columns; ubuf holds exactly the records' bytes (rec_off into it)."""
+    """One window's host copy (hbam_records_to_host: key, voffset, rec_off, block_size and the
+    records' bytes — views of the context's pinned staging, valid until the next window)."""
 
     def __init__(self, cols):
         self.cols = cols
@@ -802,7 +730,8 @@ def read_header(data, ctx):
 class BAMRecordReader:
     """BAMRecordReader.java:48-188.  initialize() opens a streamed device decode of the split
     (hbam_split_open: windows of hadoopbam.hip.window-bytes compressed bytes, the next one
-    copied while the current one decodes); nextKeyValue() walks each window's columns and
+    copied while the current one decodes); each window's records come to the host through
+    hbam_records_to_host (key, voffset, record bytes only); nextKeyValue() walks them and
     raises the reference's exception at the record where the reference raises it.  The key
     and value objects are reused, as in the reference (:53-54, :185-186)."""
 
@@ -858,10 +787,12 @@ class BAMRecordReader:
             fd = self._fd
             self._gen = self.ctxt.split_stream_reader(lambda off, n: os.pread(fd, n, off), len(data),
                                                       split.getStartVirtualOffset(),
-                                                      split.getEndVirtualOffset(), h["n_ref"], window)
+                                                      split.getEndVirtualOffset(), h["n_ref"], window,
+                                                      host="records")
         else:
             self._gen = self.ctxt.split_stream(data, split.getStartVirtualOffset(),
-                                               split.getEndVirtualOffset(), h["n_ref"], window)
+                                               split.getEndVirtualOffset(), h["n_ref"], window,
+                                               host="records")
         self.dec = None
         self.i = self.n = 0
         self.status = 0
@@ -895,7 +826,9 @@ class BAMRecordReader:
         i = self.i
         self.i += 1
         self.key.set(int(self.dec.cols["key"][i]))
-        self.record.set(BAMRecordView(self.dec, i))
+        # the value is the lazily decoded record over the record's bytes, as the reference's codec
+        # builds it (:172-188)
+        self.record.set(BAMRecordBytes(self.dec.record_bytes(i)))
         return True
 
     def getCurrentKey(self):

@@ -497,19 +497,41 @@ class SamFileHeaderMerger:
         return SAMFileHeader(b"\n".join(lines) + b"\n", self.merged_refs)
 
 
-def correct_for_merging(ctx, cols, merger, input_index):
+def correct_for_merging(ctx, cols, merger, input_index, raise_error=True):
     """SortRecordReader.nextKeyValue's Utils.correctSAMRecordForMerging over a decoded split
-    (device hbam_columns, modified in place) of input `input_index` (hbam_merge_remap)."""
+    (device hbam_columns, modified in place) of input `input_index` (hbam_merge_remap).  Returns
+    the first record whose merged index lies outside its own dictionary (or None); raises there
+    unless raise_error is False."""
     if not merger.has_merged_sequence_dictionary:
-        return
+        return None
     m = np.ascontiguousarray(merger.ref_maps[input_index], np.int32)
     bad = C.c_uint64(0)
     rc = ctx.L.hbam_merge_remap(ctx.h, C.byref(cols), C.c_void_p(m.ctypes.data), len(m), C.byref(bad))
     if rc:
         raise RuntimeError("hbam_merge_remap failed (%d): %s" % (rc, ctx.last_error()))
-    if bad.value != (1 << 64) - 1:
-        raise ValueError("Reference index not found in sequence dictionary (record %d of input %d: "
-                         "SAMRecord.setReferenceIndex against the input's header)" % (bad.value, input_index))
+    if bad.value == (1 << 64) - 1:
+        return None
+    if raise_error:
+        _raise_refid(bad.value, input_index)
+    return int(bad.value)
+
+
+def _raise_refid(record, input_index):
+    raise ValueError("Reference index not found in sequence dictionary (record %d of input %d: "
+                     "SAMRecord.setReferenceIndex against the input's header)" % (record, input_index))
+
+
+def correct_split(ctx, cols, merger, input_index):
+    """Both halves of correctSAMRecordForMerging (cli/Utils.java:286-324) in the reference's
+    per-record order: record r's dictionary step, then its group step.  When the dictionary step
+    refuses record `bad`, the records before it still get their group rewrite, and an exception
+    the group step raises at an earlier record is the one the job sees."""
+    bad = correct_for_merging(ctx, cols, merger, input_index, raise_error=False)
+    if bad is not None:
+        cols.n_records = bad
+    correct_groups(ctx, cols, merger, input_index)
+    if bad is not None:
+        _raise_refid(bad, input_index)
 
 
 def correct_groups(ctx, cols, merger, input_index):
@@ -550,8 +572,7 @@ def sort_inputs(ctx, inputs, ops=None, sort_order="coordinate"):
         rc, cols = ctx.decode_split_device(data, h["first_voffset"], (n << 16) | 0xffff, h["n_ref"])
         if rc or cols.status:
             raise RuntimeError("decode of input %d failed rc=%d status=%d: %s" % (i, rc, cols.status, ctx.last_error()))
-        correct_for_merging(ctx, cols, merger, i)
-        correct_groups(ctx, cols, merger, i)
+        correct_split(ctx, cols, merger, i)
         runs.append(ops.run_from_columns(cols))
     if len(runs) == 1:
         return merger.getMergedHeader(), runs[0]

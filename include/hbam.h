@@ -188,6 +188,15 @@ int hbam_decode_split(hbam_ctx* ctx, const uint8_t* comp, int on_device, uint64_
                       uint64_t comp_len, uint64_t file_len, uint64_t v_start, uint64_t v_end,
                       int32_t n_ref, hbam_columns* out);
 int hbam_columns_to_host(hbam_ctx* ctx, const hbam_columns* dev, hbam_columns* host);
+/* Records-only host copy for the drop-in reader: BAMRecordReader.nextKeyValue
+ * (BAMRecordReader.java:172-188) hands out one record at a time and needs only its bytes, its key
+ * and (getProgress, :157-168) its virtual offset.  host gets n_records, status, err_record, key,
+ * voffset, block_size, rec_off (relative to host->ubuf) and ubuf = exactly the records' bytes
+ * (each record's block_size field + record); every other pointer is NULL.  The arrays live in
+ * pinned host memory owned by the context, valid until the next hbam_records_to_host or
+ * hbam_destroy on it (never pass them to hbam_free_host_columns).  Copies 28 B per record plus
+ * the record bytes (columns_to_host copies every pool too: about twice as much). */
+int hbam_records_to_host(hbam_ctx* ctx, const hbam_columns* dev, hbam_columns* host);
 /* Streamed split read: BAMRecordReader over FileVirtualSplit
  * [v_start, v_end) of a file the caller holds in host memory (e.g. mmap; only the split's
  * windows are copied, see hbam_split_open_reader for the bound), decoded in windows

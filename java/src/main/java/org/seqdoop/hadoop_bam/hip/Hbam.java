@@ -38,6 +38,9 @@ public final class Hbam implements AutoCloseable {
   static final MethodHandle COLUMNS_TO_HOST = fn("hbam_columns_to_host",
       FunctionDescriptor.of(I, A, A, A));
   static final MethodHandle FREE_HOST = fn("hbam_free_host_columns", FunctionDescriptor.ofVoid(A));
+  // the drop-in reader's copy: key, voffset, rec_off, block_size + record bytes (context-owned, pinned)
+  static final MethodHandle RECORDS_TO_HOST = fn("hbam_records_to_host",
+      FunctionDescriptor.of(I, A, A, A));
   static final MethodHandle SPLIT_OPEN = fn("hbam_split_open",
       FunctionDescriptor.of(A, A, A, J, J, J, I, J));
   static final MethodHandle SPLIT_NEXT = fn("hbam_split_next", FunctionDescriptor.of(I, A, A));

@@ -120,11 +120,11 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     return cols.get(ValueLayout.ADDRESS, Hbam.offsetOf(f)).reinterpret(Math.max(bytes, 1));
   }
 
-  /** The next window's records (hbam_split_next + hbam_columns_to_host); false at the end. */
+  /** The next window's records (hbam_split_next + hbam_records_to_host); false at the end. */
   private boolean nextWindow() {
     long bad = -1;  // first record hbam_merge_remap refuses (HipSortRecordReader only)
     try {
-      if (hostLive) { Hbam.FREE_HOST.invokeExact(host); hostLive = false; }
+      hostLive = false;  // the previous window's host copy is the context's staging: reused below
       final int rc = (int) Hbam.SPLIT_NEXT.invokeExact(stream, dev);
       if (rc < 0) {
         if (source.failure() != null) throw new RuntimeIOException(source.failure());
@@ -140,7 +140,12 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
           bad = b.get(ValueLayout.JAVA_LONG, 0);
         }
       }
-      if (groupTable != null && (mergeMap == null || bad < 0)) {
+      if (groupTable != null) {
+        // correctSAMRecordForMerging runs per record (cli/Utils.java:286-324): the records before
+        // the one setReferenceIndex refuses still get their group rewrite, so the rewrite covers
+        // [0, bad) and an exception it raises at an earlier record is the one thrown
+        if (bad >= 0 && bad < dev.get(ValueLayout.JAVA_LONG, Hbam.offsetOf("n_records")))
+          dev.set(ValueLayout.JAVA_LONG, Hbam.offsetOf("n_records"), bad);
         try (Arena a = Arena.ofConfined()) {
           final MemorySegment t = a.allocateFrom(ValueLayout.JAVA_BYTE, groupTable);
           final MemorySegment st = a.allocate(ValueLayout.JAVA_INT), er = a.allocate(ValueLayout.JAVA_LONG);
@@ -149,8 +154,10 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
           groupStatus = st.get(ValueLayout.JAVA_INT, 0);
         }
       }
-      final int rc2 = (int) Hbam.COLUMNS_TO_HOST.invokeExact(hbam.context(), dev, host);
-      if (rc2 != Hbam.OK) throw new RuntimeIOException("hbam_columns_to_host: " + hbam.lastError());
+      // only what nextKeyValue reads: key, voffset, rec_off, block_size and the record bytes, into
+      // the context's pinned staging (hbam_records_to_host; no pool crosses PCIe)
+      final int rc2 = (int) Hbam.RECORDS_TO_HOST.invokeExact(hbam.context(), dev, host);
+      if (rc2 != Hbam.OK) throw new RuntimeIOException("hbam_records_to_host: " + hbam.lastError());
       hostLive = true;
     } catch (RuntimeException e) {
       throw e;
@@ -159,17 +166,17 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     }
     n = host.get(ValueLayout.JAVA_LONG, Hbam.offsetOf("n_records"));
     status = host.get(ValueLayout.JAVA_INT, Hbam.offsetOf("status"));
-    if (groupStatus != Hbam.OK) {  // the rewrite stopped at record n (dv holds the records before it)
-      status = groupStatus;
-      groupStatus = Hbam.OK;
-    }
-    if (status != Hbam.OK) last = true;
-    if (mergeMap != null && bad >= 0 && bad < n) {
+    final int gs = groupStatus;
+    groupStatus = Hbam.OK;
+    if (gs != Hbam.OK) {
+      // the rewrite stopped at record n (dv holds the records before it), before any `bad`
+      status = gs;
+    } else if (mergeMap != null && bad >= 0 && bad <= n) {
       // SAMRecord.setReferenceIndex against the record's own header throws here (:286-313)
       n = bad;
       status = Hbam.EREFID;
-      last = true;
     }
+    if (status != Hbam.OK) last = true;
     i = 0;
     keys = ptr(host, "key", 8 * n);
     voffs = ptr(host, "voffset", 8 * n);
@@ -212,7 +219,6 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
 
   @Override public void close() throws IOException {
     try {
-      if (hostLive) Hbam.FREE_HOST.invokeExact(host);
       if (stream != null && stream.address() != 0) Hbam.SPLIT_CLOSE.invokeExact(stream);
       if (source != null) source.close();
     } catch (Throwable t) {

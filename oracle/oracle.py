@@ -674,6 +674,10 @@ def sort_merged(datas):
         if did:
             pay, keys, bad = correct_payloads(pay, off, keys, [names.index(n) for n, _ in dic])
             if bad >= 0:
+                # correctSAMRecordForMerging runs per record (cli/Utils.java:286-324, called from
+                # SortRecordReader.nextKeyValue, Sort.java:279-295): the records before `bad` get
+                # their group step first, and an exception there comes first
+                rewrite_group_tags(pay, off[:bad + 1], groups, fi)
                 raise ValueError("input %d record %d: index outside its dictionary" % (fi, bad))
         pay, off = rewrite_group_tags(pay, off, groups, fi)
         for i in range(cols["n"]):

@@ -126,10 +126,11 @@ def redictionary_bam(data, prepend=((b"chrNEW", 5000),), drop_last=1):
     return np.frombuffer(bgzf_pack(b"".join(out)), np.uint8).copy(), refs, new_refs
 
 
-def regroup_bam(data, text_fn, rg_fn):
+def regroup_bam(data, text_fn, rg_fn, ref_fn=None):
     """A copy of a BAM with its header text replaced by text_fn(text) and each record's first RG
     tag replaced by rg_fn(i, value): None drops the tag, bytes = a new Z value, (type, raw) any
-    typed value (multi-input Sort group-collision tests)."""
+    typed value (multi-input Sort group-collision tests); ref_fn(i, refID) -> the record's new
+    refID (and mate refID, where placed)."""
     import struct
     import oracle
     u = bam_stream(data)
@@ -162,7 +163,12 @@ def regroup_bam(data, text_fn, rg_fn):
                     aux += tag + b"Z" + new + b"\0"
             else:
                 aux += tag + ty + val
-        body = r[4:vstart] + aux
-        out.append(struct.pack("<i", len(body)) + body)
+        body = bytearray(r[4:vstart] + aux)
+        if ref_fn is not None:
+            for o in (0, 20):  # refID, mate refID (body offsets)
+                v = struct.unpack_from("<i", body, o)[0]
+                if v >= 0:
+                    struct.pack_into("<i", body, o, ref_fn(i, v))
+        out.append(struct.pack("<i", len(body)) + bytes(body))
         i += 1
     return np.frombuffer(bgzf_pack(b"".join(out)), np.uint8).copy()

@@ -795,6 +795,40 @@ def test_split_local_reader_reads_the_split_not_the_file(gpu_ctx, oracle_mod):
         assert rd.total() < L // 4
 
 
+@pytest.mark.parametrize("name", ["small_pe.bam", "edge_uniform_long.bam", "edge_unsorted_l1.bam"])
+def test_records_to_host_is_what_the_reader_hands_out(gpu_ctx, oracle_mod, name):
+    """hbam_records_to_host (the drop-in reader's copy, BAMRecordReader.java:172-188): per window,
+    key, voffset, block_size and exactly the records' bytes (rec_off into them) — equal to the
+    oracle's — and nothing else: 28 B per record + the record bytes cross to the host."""
+    data = _load(name)
+    h = oracle_mod.read_header(data)
+    ref = oracle_mod.read_split(data, h["first_voffset"], _whole(data))
+    pay, off = oracle_mod.record_payloads(ref)
+    got_k, got_v, got_b, recs, d2h = [], [], [], [], 0
+    for w in gpu_ctx.split_stream(data, h["first_voffset"], _whole(data), h["n_ref"], window_bytes=64 << 10,
+                                  host="records"):
+        n = w["n"]
+        got_k.append(w["key"].copy())
+        got_v.append(w["voffset"].copy())
+        got_b.append(w["block_size"].copy())
+        u = w["ubuf"]
+        assert len(u) == int(np.sum(w["block_size"].astype(np.int64) + 4)), "ubuf holds only the records"
+        for i in range(n):
+            r = int(w["rec_off"][i])
+            recs.append(u[r:r + 4 + int(w["block_size"][i])].tobytes())
+        assert w["d2h_bytes"] == 28 * n + len(u)
+        d2h += w["d2h_bytes"]
+        last = w
+    assert last["status"] == ref["status"]
+    assert np.array_equal(np.concatenate(got_k), ref["key"])
+    assert np.array_equal(np.concatenate(got_v), ref["voffset"])
+    assert np.array_equal(np.concatenate(got_b), ref["block_size"])
+    assert b"".join(recs) == pay.tobytes()
+    assert d2h == 28 * ref["n"] + len(pay)
+    if name == "small_pe.bam":  # 150 bp PE records: within 1.1 x the record bytes
+        assert d2h <= 1.1 * len(pay)
+
+
 def test_windowed_decode_comp_base(gpu_ctx, oracle_mod):
     """hbam_decode_split with comp_base != 0: a window [c, c+W) of the file decodes the same
     records as the whole buffer up to the window's EMORE, whose voffset[n] is the resume point."""

@@ -144,6 +144,7 @@ def sort_parity(ctx, ops, dev, data, h, run, a):
     m = int(cols.n_records)
     ident = torch.arange(m, dtype=torch.int32, device="cuda")
     dv = torch.empty(m, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # libhbam runs on its own stream: torch's arange must have landed
     assert ctx.L.hbam_permute(ctx.h, C.cast(cols.voffset, C.c_void_p), 8, C.c_void_p(ident.data_ptr()), m,
                               C.c_void_p(dv.data_ptr())) == 0
     del ident
