@@ -175,7 +175,7 @@ def parity_at_size(ctx, buf, dbuf, n_splits, seed, threads, whole=None):
         if ge or go == int(ends[i]):
             res[i] = (go, None)
             return
-        r = oracle.read_split(sub, go, (int(ends[i]) << 16) | 0xffff)
+        r = oracle.read_split(sub, go, (int(ends[i]) << 16) | 0xffff, n_ref=N_REF)
         res[i] = (go, r)
 
     ths = [threading.Thread(target=ref_one, args=(i,)) for i in range(n_splits)]

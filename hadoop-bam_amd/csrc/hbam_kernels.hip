@@ -711,6 +711,11 @@ __global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* _
 #endif
 }
 
+#include "resolve_units.h"
+#ifndef HBAM_RS_UNITS
+#define HBAM_RS_UNITS 0  // LZ77 pass: k_resolve_units (16-byte units, aligned masked writes) instead of k_resolve
+#endif
+
 // CRC-32 (IEEE, reflected 0xEDB88320) of each inflated block, slice-by-4 tables in LDS.
 __global__ __launch_bounds__(256) void k_crc32(const BlockRec* __restrict__ blk,
                                                const uint64_t* __restrict__ uoff, uint32_t nblk,

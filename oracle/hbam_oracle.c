@@ -505,12 +505,25 @@ out:
 
 /* ------------------------------------------------------------------------------ */
 /* BAMRecordReader.initialize (:108-151) + nextKeyValue (:172-188).                  */
+static int read_split_body(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end,
+                           int check_crc, int32_t n_ref, or_record_cb cb, void* user, or_read_result* res);
 int or_read_split(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end,
                   int check_crc, or_record_cb cb, void* user, or_read_result* res) {
   memset(res, 0, sizeof *res);
   or_header h;
   int rc = or_read_header(f, len, &h);
   if (rc) { res->status = rc; return rc; }
+  return read_split_body(f, len, v_start, v_end, check_crc, h.n_ref, cb, user, res);
+}
+
+/* The same loop when the header was read elsewhere (BAMRecordReader.initialize reads it from the
+ * start of the file, :128-130): f is a window of the file holding the split's blocks (a shard of a
+ * byte-range-sharded file), voffsets relative to the window, n_ref the header's dictionary size. */
+static int read_split_body(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end,
+                           int check_crc, int32_t n_ref, or_record_cb cb, void* user, or_read_result* res) {
+  int rc;
+  memset(res, 0, sizeof *res);
+  struct { int32_t n_ref; } h = {n_ref};
   ostream s = {f, (int64_t)len, 0};
   bcis* b = bcis_new(&s, check_crc);
   if (!b) { res->status = OR_ENOMEM; return OR_ENOMEM; }
@@ -1057,18 +1070,26 @@ static int cols_cb(void* user, const or_record* r) {
 }
 #undef GROW
 
-int or_read_split_cols(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end,
-                       int check_crc, int keep_var, or_cols* out) {
+int or_read_split_cols_nref(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end,
+                            int check_crc, int keep_var, int32_t n_ref, or_cols* out) {
   memset(out, 0, sizeof *out);
   cols_ctx x = {out, keep_var, 0};
   or_read_result res;
-  or_read_split(f, len, v_start, v_end, check_crc, cols_cb, &x, &res);
+  if (n_ref < 0)
+    or_read_split(f, len, v_start, v_end, check_crc, cols_cb, &x, &res);
+  else
+    read_split_body(f, len, v_start, v_end, check_crc, n_ref, cols_cb, &x, &res);
   out->status = x.oom ? OR_ENOMEM : res.status;
   out->err_record = res.err_record;
   if (out->n == 0 && out->var_off == NULL) {
     out->var_off = (uint64_t*)calloc(1, sizeof(uint64_t));
   }
   return out->status;
+}
+
+int or_read_split_cols(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end,
+                       int check_crc, int keep_var, or_cols* out) {
+  return or_read_split_cols_nref(f, len, v_start, v_end, check_crc, keep_var, -1, out);
 }
 
 void or_cols_free(or_cols* c) {

@@ -148,6 +148,10 @@ typedef struct or_cols {
 
 int or_read_split_cols(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end,
                        int check_crc, int keep_var, or_cols* out);
+/* the same with the header read elsewhere: f is a window of the file (a shard), n_ref >= 0 the
+ * header's dictionary size (n_ref < 0: read the header from f, as or_read_split_cols) */
+int or_read_split_cols_nref(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end,
+                            int check_crc, int keep_var, int32_t n_ref, or_cols* out);
 void or_cols_free(or_cols* c);
 
 

@@ -56,6 +56,9 @@ def lib():
         L.or_splitting_index.argtypes = [u8p, C.c_uint64, C.c_int32, C.c_void_p, C.c_uint64]
         L.or_bgzf_block_index.restype = C.c_int64
         L.or_bgzf_block_index.argtypes = [u8p, C.c_uint64, C.c_int32, C.c_void_p, C.c_uint64]
+        L.or_read_split_cols_nref.restype = C.c_int
+        L.or_read_split_cols_nref.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_int,
+                                              C.c_int32, C.POINTER(OrCols)]
         L.or_read_split_cols.restype = C.c_int
         L.or_read_split_cols.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_int,
                                          C.POINTER(OrCols)]
@@ -158,11 +161,16 @@ def read_header(data):
                 first_voffset=h.first_voffset)
 
 
-def read_split(data, v_start, v_end, check_crc=False, keep_var=True):
-    """BAMRecordReader over one FileVirtualSplit -> dict of numpy columns."""
+def read_split(data, v_start, v_end, check_crc=False, keep_var=True, n_ref=None):
+    """BAMRecordReader over one FileVirtualSplit -> dict of numpy columns.  n_ref given: `data` is a
+    window of the file (a byte-range shard, voffsets relative to it) whose header was read elsewhere."""
     a, p = _buf(data)
     c = OrCols()
-    lib().or_read_split_cols(p, len(a), v_start, v_end, int(check_crc), int(keep_var), C.byref(c))
+    if n_ref is None:
+        lib().or_read_split_cols(p, len(a), v_start, v_end, int(check_crc), int(keep_var), C.byref(c))
+    else:
+        lib().or_read_split_cols_nref(p, len(a), v_start, v_end, int(check_crc), int(keep_var), int(n_ref),
+                                      C.byref(c))
     n = int(c.n)
     out = dict(n=n, status=int(c.status), err_record=int(c.err_record))
     for name, dt in FIXED_FIELDS:

@@ -18,6 +18,7 @@
 #   crc                  tools/check_inflate_crc.py
 #   calib                rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/pmc_calib (known bytes per shape)
 #   py,SCRIPT[,ARGS..]   any repo script (ARGS separated by ',')
+#   pyo,NAME,SCRIPT[,ARGS..]  the same, output to NAME.txt
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$1
@@ -42,7 +43,8 @@ for spec in "$@"; do
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --parity-splits 0 > $O/bench_prof.json 2> $O/prof.err; r=$? ;;
     pmc)  # pmc,COUNTERS[,SIZE[,LIB]]: one counter pass over a decode (csv per dispatch)
-      timeout -s KILL 300 rocprofv3 --pmc ${a1//+/ } -d $O/pmc_${a1//+/_} -o run --output-format csv -- python3 tools/ab_decode.py --size ${a2:-2e9} --reps 1 --digest 0 --libs ${a3:-libhbam.so} > $O/pmc_${a1//+/_}.txt 2>&1; r=$? ;;
+      P=$O/pmc_${a1//+/_}${a3:+_$a3}
+      timeout -s KILL 300 rocprofv3 --pmc ${a1//+/ } -d $P -o run --output-format csv -- python3 tools/ab_decode.py --size ${a2:-2e9} --reps 1 --digest 0 --libs ${a3:-libhbam.so} > $P.txt 2>&1; r=$? ;;
     pmcbytes)  # pmcbytes[,SIZE]: FETCH_SIZE and WRITE_SIZE passes over one decode -> tools/pmc_summarize.py
       timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmcb_fetch -o run --output-format csv -- python3 tools/ab_decode.py --size ${a1:-10e9} --reps 1 --digest 0 --libs libhbam.so > $O/pmcb_fetch.txt 2>&1 &&
       timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d $O/pmcb_write -o run --output-format csv -- python3 tools/ab_decode.py --size ${a1:-10e9} --reps 1 --digest 0 --libs libhbam.so > $O/pmcb_write.txt 2>&1; r=$?
@@ -69,8 +71,11 @@ for spec in "$@"; do
       [ $r -eq 0 ] && python3 tools/pmc_calib.py $O/calib.txt $(ls $O/calib_fetch/*counter_collection.csv $O/calib_fetch/*/*counter_collection.csv 2>/dev/null | head -1) $(ls $O/calib_write/*counter_collection.csv $O/calib_write/*/*counter_collection.csv 2>/dev/null | head -1) $O/calib.json > $O/calib_summary.txt 2>&1 ;;
     crc)
       timeout -k 10 900 python -u tools/check_inflate_crc.py > $O/crc.txt 2>&1; r=$? ;;
+    pyo)
+      rest="${spec#pyo,$a1,$a2}"; rest="${rest#,}"; ARGS=(); [ -n "$rest" ] && IFS=, read -r -a ARGS <<< "$rest"
+      timeout -k 10 900 python -u "$a2" "${ARGS[@]}" > $O/$a1.txt 2>&1; r=$? ;;
     py)
-      IFS=, read -r -a ARGS <<< "${spec#py,$a1}"
+      rest="${spec#py,$a1}"; rest="${rest#,}"; ARGS=(); [ -n "$rest" ] && IFS=, read -r -a ARGS <<< "$rest"
       timeout -k 10 900 python -u "$a1" "${ARGS[@]}" > $O/$(basename $a1 .py).txt 2>&1; r=$? ;;
     *)
       echo "unknown step $spec" >> $O/steps.log; r=2 ;;

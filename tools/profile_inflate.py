@@ -18,9 +18,10 @@ ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--seed", type=int, default=2)
 ap.add_argument("--prof", action="store_true",
                 help="use libhbam_prof.so (built with -DHBAM_PROF) and print per-block cycle stats")
+ap.add_argument("--prof-lib", default="libhbam_prof.so", help="--prof: the profiling build to load")
 a = ap.parse_args()
 if a.prof:
-    os.environ["HBAM_LIB"] = os.path.join(ROOT, "hadoop-bam_amd", "libhbam_prof.so")
+    os.environ["HBAM_LIB"] = os.path.join(ROOT, "hadoop-bam_amd", a.prof_lib)
     os.environ["HBAM_INFLATE_SLICES"] = "1"  # per-block prof slots are indexed per launch
     os.environ["HBAM_WAVE_MAX_BLOCKS"] = "0"  # the stamps are in the lane-per-block Huffman pass
 g = genbam.generate(target_bytes=int(a.size), seed=a.seed, threads=16)
@@ -40,7 +41,9 @@ h = ctx.parse_header(d[:len(data)])
 for _ in range(a.reps):
     rc, cols = ctx.decode_split_device(d[:len(data)], h["first_voffset"], (len(data) << 16) | 0xffff,
                                        h["n_ref"])
-    assert rc == 0 and cols.status == 0 and cols.n_records == g.n_records
+    if not (rc == 0 and cols.status == 0 and cols.n_records == g.n_records):
+        raise SystemExit("decode failed: rc %d status %d records %d of %d: %s" % (
+            rc, cols.status, cols.n_records, g.n_records, ctx.last_error()))
     print({k: round(v, 3) if isinstance(v, float) else v for k, v in ctx.timing().items()}, flush=True)
 
 if a.prof:

@@ -11,8 +11,9 @@ grouped ncclSend/ncclRecv per peer over xGMI); on gloo (the one-GPU rehearsal) t
 all_to_all of hadoop_bam/sort.py.
 
 Parity of the timed output, outside the timed region:
-  * order: every rank's records in strictly increasing (key, voffset) order, and across ranks the
-    last record of rank r before the first of rank r+1 (the concatenation is the total order);
+  * order: every rank's records in (key, voffset) order, and across ranks the last record of rank r
+    before the first of rank r+1 (the concatenation is the total order; a record read by both
+    neighbouring splits — its block starts exactly at a split boundary — appears twice, adjacent);
   * permutation + payload: each record gets a fingerprint of its payload bytes (position-weighted,
     computed on the device); the sums over records of (voffset hash) and (fingerprint x voffset
     hash), all-reduced, equal between the decoded splits (in file order) and the sorted output, and
@@ -134,7 +135,9 @@ def run(ctx, dist, rank, world, size, seed, threads, dev, cdev, n_ref, steps=2, 
     tp = time.time()
     n = out.n
     k, v = out.keys, out.voffset
-    order_ok = bool(((k[1:] > k[:-1]) | ((k[1:] == k[:-1]) & (v[1:] > v[:-1]))).all()) if n > 1 else True
+    # (key, voffset) non-decreasing: equal pairs are the records of a block starting exactly at a
+    # split boundary, which both neighbouring splits read (as the reference does)
+    order_ok = bool(((k[1:] > k[:-1]) | ((k[1:] == k[:-1]) & (v[1:] >= v[:-1]))).all()) if n > 1 else True
     ends = torch.tensor([n, int(k[0]) if n else 0, int(v[0]) if n else 0, int(k[-1]) if n else 0,
                          int(v[-1]) if n else 0], dtype=torch.int64, device=cdev)
     ends_all = [torch.zeros_like(ends) for _ in range(world)]
@@ -144,7 +147,7 @@ def run(ctx, dist, rank, world, size, seed, threads, dev, cdev, n_ref, steps=2, 
     for r in range(world):
         if e[r][0] == 0:
             continue
-        if last is not None and not (last[0] < e[r][1] or (last[0] == e[r][1] and last[1] < e[r][2])):
+        if last is not None and not (last[0] < e[r][1] or (last[0] == e[r][1] and last[1] <= e[r][2])):
             boundary_ok = False
         last = (e[r][3], e[r][4])
     s_out = _stats(v, fingerprints(out.payload, out.offsets))
@@ -186,7 +189,7 @@ def run(ctx, dist, rank, world, size, seed, threads, dev, cdev, n_ref, steps=2, 
     def chk(ix):
         for i in ix:
             rv = int(vo[i]) - (off << 16)
-            ref = oracle.read_split(sub, rv, rv + 1)
+            ref = oracle.read_split(sub, rv, rv + 1, n_ref=n_ref)
             okk = ref["n"] == 1 and oracle.record_payloads(ref)[0].tobytes() == host_pay[int(i)]
             if not okk:
                 with lock:
