@@ -543,13 +543,8 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
       }
       if (si + 1 == ns) HIPCHK(c, hipEventRecord(c->ev[11], c->stream));
       k_edge_merge<<<grid_for(2 * n, 256), 256, 0, rs>>>(blk + lo, uoff + lo, (uint32_t)n, ubuf, edges + 32 * lo);
-#if HBAM_RS_UNITS
       k_resolve_units<<<(uint32_t)n, 64, 0, rs>>>(blk + lo, uoff + lo, (uint32_t)n, ubuf, bitmap + lo * BITMAP_WORDS,
                                                   tails + 2 * lo, st + lo);
-#else
-      k_resolve<<<(uint32_t)n, 64, 0, rs>>>(blk + lo, uoff + lo, (uint32_t)n, ubuf, bitmap + lo * BITMAP_WORDS,
-                                            tails + 2 * lo, st + lo);
-#endif
     }
     if (ns > 1) {
       HIPCHK(c, hipEventRecord(c->slice_ev[HBAM_MAX_SLICES], c->stream2));
@@ -2437,11 +2432,7 @@ extern "C" int hbam_resolve_tokens(hbam_ctx* c, uint8_t* io, uint32_t isize, con
   HIPCHK(c, hipMemcpyAsync(bm, bitmap, 4ull * ((isize + 31u) / 32u), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(tails, tl, sizeof tl, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(st, &zero, 4, hipMemcpyHostToDevice, c->stream));
-#if HBAM_RS_UNITS
   k_resolve_units<<<1, 64, 0, c->stream>>>(blk, uoff, 1, ub, bm, tails, st);
-#else
-  k_resolve<<<1, 64, 0, c->stream>>>(blk, uoff, 1, ub, bm, tails, st);
-#endif
   HIPCHK(c, hipGetLastError());
   int32_t hs = 0;
   HIPCHK(c, hipMemcpyAsync(&hs, st, 4, hipMemcpyDeviceToHost, c->stream));

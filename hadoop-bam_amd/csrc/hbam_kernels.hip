@@ -227,9 +227,9 @@ __global__ void k_verify_chain(const uint8_t* __restrict__ comp, const uint64_t*
 //    decode with wave-uniform input epochs; literals land in ubuf, each match leaves a
 //    3-byte descriptor in its hole and a bit in the block's match-start bitmap (TSink,
 //    inflate_tok.h).  LDS: per lane 288 + 32 u8 symbol slots.
-//  k_resolve (phase 2): one wave per block; the block's output is staged in LDS (64 KiB),
-//    matches are executed in order in batches of mutually independent copies (a match
-//    whose source ends before the first pending destination), then written back.
+//  k_resolve_units (phase 2, LZ77): one wave per block walks it in 1 KiB stretches staged in
+//    LDS; every match is cut into <= 16-byte units, copied all at once when their source is
+//    final, in dataflow rounds otherwise (resolve_units.h).
 // ------------------------------------------------------------------------------------
 #ifdef HBAM_PROF
 // Profiling build only (libhbam_prof.so, tools/profile_inflate.py --prof): per-block cycle
@@ -369,7 +369,6 @@ __global__ void k_edge_merge(const BlockRec* __restrict__ blk, const uint64_t* _
   for (uint32_t r = lo; r < hi; ++r) base[r] = src[r & 15u];
 }
 
-// LZ77 resolution of one block (phase 2 of the batched inflate); see resolve_dev.h.
 // one 16-byte column of a resolved stretch -> ubuf (bytewise where it overlaps a neighbour block)
 __device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64_t a, uint64_t base,
                                               uint64_t aend, const uint4 v) {
@@ -382,339 +381,8 @@ __device__ __forceinline__ void rs_write_back(uint8_t* __restrict__ ubuf, uint64
     }
   }
 }
-#ifndef HBAM_RS_WAVES
-// waves per SIMD asked of the register allocator: 8 = the hardware maximum, which the 4.9 KiB of
-// LDS per block also allows (VGPRs 75 -> 64, 2 spilled): k_resolve 47.4 -> 42.6 ms at 10 GB
-#define HBAM_RS_WAVES 8
-#endif
-#ifndef HBAM_RS_DSC_AL
-#define HBAM_RS_DSC_AL 1  // aligned descriptor reads: 21.5 -> 21.0 ms at 5 GB (profiles/r04/ab/resolve_depmask_dscal_5g.txt)
-#endif
-#ifndef HBAM_RS_DEPMASK
-#define HBAM_RS_DEPMASK 1  // dependency masks for <= 64 ordered matches: 21.5 -> 19.6 ms; both 19.1 (same file)
-#endif
-__global__ __launch_bounds__(64, HBAM_RS_WAVES) void k_resolve(const BlockRec* __restrict__ blk,
-                                                const uint64_t* __restrict__ uoff, uint32_t nblk,
-                                                uint8_t* __restrict__ ubuf,
-                                                const uint32_t* __restrict__ bitmap,
-                                                const uint32_t* __restrict__ tails,
-                                                int32_t* __restrict__ status) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_buf[RS_BUF];
-  // match records, packed: index into s_pos (9 bits) | len-3 << 9 | dist-1 << 17 (u32 instead of
-  // the unpacked u64: 1.4 KiB less LDS per wave); pre matches from the front, ordered from the back
-  __shared__ uint32_t s_rec[RS_MAXM];
-  __shared__ uint16_t s_pos[RS_MAXM];
-  __shared__ uint64_t s_sel[8];
-  __shared__ uint32_t s_pend[RS_PW];
-  const uint32_t b = blockIdx.x;
-  const uint32_t lane = threadIdx.x;
-  if (b >= nblk) return;
-#ifdef HBAM_PROF
-  const uint64_t pr0 = PROF_RT(), pc0 = PROF_CLK();
-  uint64_t p_desc = 0, p_bat = 0, n_bat = 0, n_m = 0, p_st = 0, p_pre = 0, p_wb = 0;
-#endif
-  if (status[b] != INF_OK) return;
-  const uint32_t isize = blk[b].isize;
-  if (isize == 0 || isize > 65536u) return;
-  const uint32_t* bm = bitmap + (uint64_t)b * BITMAP_WORDS;
-  const uint32_t nwords = (isize + 31u) >> 5;
-  const uint32_t tail0 = tails[2 * (uint64_t)b];
-  bool tail_bad = false;
-  {
-    uint32_t any = 0;
-    for (uint32_t w = lane; w < nwords; w += 64) any |= bm[w];
-    if (!__any(any != 0) && !(tail0 & 0x80000000u)) return;
-  }
-  if (lane < 8) {  // v_perm selectors: byte j of the period-d pattern = byte (j mod d)
-    const uint32_t d = lane ? lane : 1u;
-    uint64_t sel = 0;
-    for (uint32_t j = 0; j < 8; ++j) sel |= (uint64_t)(j % d) << (8 * j);
-    s_sel[lane] = sel;
-  }
-  const uint64_t base = uoff[b];
-  const uint64_t abase = base & ~15ULL;
-  const uint32_t a0 = (uint32_t)(base - abase);
-  const uint64_t aend = base + isize;
-  // Stretch k writes back global [abase + k*RS_S, +RS_S) = block offsets [k*RS_S - a0, ..): a
-  // block that does not start 16-aligned needs one more stretch than ISIZE alone when its
-  // last bytes fall past nstr*RS_S - a0 (the matches listed for stretch k, positions
-  // [k*RS_S, (k+1)*RS_S), reach a0 bytes into the next stretch's bytes).
-  const uint32_t nstr = (a0 + isize + RS_S - 1) / RS_S;
-  // raw stretch k occupies global [abase + k*RS_S, +RS_S) (16-byte chunks, 2 per lane)
-  auto load_raw = [&](uint32_t k, uint4& r0, uint4& r1) {
-    const uint64_t g = abase + (uint64_t)k * RS_S + 16u * lane;
-    if (k < nstr) {
-      r0 = *(const uint4*)(ubuf + g);
-      if (RS_C == 2) r1 = *(const uint4*)(ubuf + g + 1024);
-    }
-  };
-  uint4 ra0 = make_uint4(0, 0, 0, 0), ra1 = ra0, rb0 = ra0, rb1 = ra0;
-  load_raw(0, ra0, ra1);
-  load_raw(1, rb0, rb1);
-  *(uint4*)(s_buf + RS_W + 16u * lane) = ra0;
-  if (RS_C == 2) *(uint4*)(s_buf + RS_W + 1024 + 16u * lane) = ra1;
-  *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = rb0;
-  if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = rb1;
-  load_raw(2, ra0, ra1);  // ra = raw[k+2] during stretch k
-  constexpr uint32_t WPS = RS_S / 32;  // bitmap words per stretch (<= 64: one per lane)
-  uint32_t wnext = (lane < WPS && lane < nwords) ? bm[lane] : 0u;
-  __syncthreads();
-#ifdef HBAM_PROF
-  p_st = PROF_CLK() - pc0;
-#endif
-  for (uint32_t k = 0; k < nstr; ++k) {
-    const uint32_t s0 = k * RS_S;
-    const uint32_t word = wnext;
-    {
-      const uint32_t wi = (k + 1) * WPS + lane;
-      wnext = (lane < WPS && k + 1 < nstr && wi < nwords) ? bm[wi] : 0u;
-    }
-    // LDS index of block offset x: x - s0 + RS_W + a0
-    const uint32_t lbase = RS_W + a0 - s0;
-#ifdef HBAM_PROF
-    const uint64_t q0 = PROF_CLK();
-#endif
-    // ---- match starts of the stretch -> s_pos (in order)
-    const uint32_t cnt = __popc(word);
-    const uint32_t incl = wave_incl_sum(cnt, lane);
-    const uint32_t total = __shfl(incl, 63);
-    {
-      uint32_t wpos = incl - cnt, bits = word;
-      while (bits) {
-        const uint32_t bit = __ffs(bits) - 1;
-        bits &= bits - 1;
-        s_pos[wpos++] = (uint16_t)(s0 + 32u * lane + bit);
-      }
-    }
-    __syncthreads();
-    // ---- descriptors -> records, split pre / ordered
-    uint32_t npre = 0, nord = 0;
-    bool bad_desc = false;
-    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      uint64_t rec = 0;
-      uint32_t pk = 0;
-      bool pre = false, ord = false;
-      if (j < total) {
-        const uint32_t p = s_pos[j];
-#if HBAM_RS_DSC_AL
-        // two dword-aligned reads + v_alignbit: a byte-aligned ds_read_b32 replays (64 cycles of
-        // the CU's LDS pipe, tools/probes/lds_align_bench.hip)
-        const uint32_t dsc = lds_rd32u(s_buf, lbase + p);
-#else
-        const uint32_t dsc = *(const uint32_t*)(s_buf + lbase + p);
-#endif
-        const uint32_t len = (dsc & 0xffu) + 3u;
-        const uint32_t dist = ((dsc >> 8) & 0xffffu) + 1u;
-        const uint32_t e = p - dist + (len < dist ? len : dist);
-        rec = (uint64_t)p | (uint64_t)len << 16 | (uint64_t)dist << 32 | (uint64_t)e << 48;
-        pk = j | (len - 3u) << 9 | (dist - 1u) << 17;
-        pre = e <= s0;
-        ord = !pre;
-        // a descriptor the Huffman pass cannot have written (source before the block, or a
-        // hole past the block end): the block's tokens are corrupt
-        bad_desc |= dist > p || p + len > isize || dist > 32768u;
-      }
-      const uint64_t mp = __ballot(pre), mo = __ballot(ord);
-      if (pre) s_rec[npre + lane_rank(mp)] = pk;
-      if (ord) s_rec[RS_MAXM - 1 - (nord + lane_rank(mo))] = pk;
-      npre += (uint32_t)__popcll(mp);
-      nord += (uint32_t)__popcll(mo);
-    }
-    if (__any(bad_desc)) {  // never copy from outside the block: report DataFormatException
-      if (lane == 0) status[b] = INF_DATA;
-      return;
-    }
-    __syncthreads();
-#ifdef HBAM_PROF
-    const uint64_t q1 = PROF_CLK();
-    p_desc += q1 - q0;
-    n_m += total;
-#endif
-    // ---- pre matches: all sources final.  LDS holds block offsets from s0 - RS_W - a0 (the
-    // previous stretch's write-back region); a source older than that is read from ubuf
-    // (stretches <= k-2, written back at least one iteration ago; the drain below makes that
-    // explicit), and a source that straddles the boundary is copied in two parts.
-    // (A/B at 10 GB without this drain: 58.8 vs 58.6 ms, so it stays)
-    if (s0 >= RS_W) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t lds_from = s0 - RS_W - a0;  // block offset of LDS index 0 (when s0 >= RS_W)
-    // (pre-match copies as 16-byte units numbered over the lanes, as the pools kernel does: a
-    // first build ran 23.4 vs 21.4 ms at 5 GB and was not pursued, profiles/r03/ab/resolve_units_5g.txt)
-    for (uint32_t j = lane; j < npre; j += 64) {
-      const uint64_t rec = rs_unpack(s_rec[j], s_pos);
-      const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
-                     dist = (uint32_t)(rec >> 32) & 0xffffu;
-      const uint32_t src = p - dist;
-      if (src + RS_W + a0 >= s0) {
-        rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
-      } else {  // dist > RS_W >= 258 >= len: no overlap with the destination
-        const uint32_t gl = (lds_from - src) < len ? (lds_from - src) : len;
-        rs_copy_glb(s_buf, lbase + p, gl, ubuf + base + src);
-        if (gl < len) rs_copy_lds(s_buf, lbase + p + gl, len - gl, dist, s_sel);
-      }
-    }
-#ifdef HBAM_PROF
-    p_pre += PROF_CLK() - q1;
-#endif
-#define HBAM_RS_UNPACK_ORD(pk) rs_unpack(pk, s_pos)
-    // ---- ordered matches: dataflow rounds.  s_pend holds one bit per byte of the stretch
-    // (+ match spill) that an ordered match has yet to write; a match is ready when no byte of
-    // its external source [p - dist, p - dist + min(len, dist)) is pending.  Every round
-    // copies all ready matches at once and clears their bits, so the rounds are the depth of
-    // the stretch's match dependency graph (the earliest pending match is always ready).
-#if HBAM_RS_DEPMASK
-    if (nord && nord <= 64u) {
-      // At most one ordered match per lane (94 % of stretches): dependencies as match-index
-      // ranges instead of a pending-byte bitmap.  Destinations are disjoint and in index order,
-      // so the ordered matches writing into match k's external source [a, e) are the index range
-      // [lo, hi): lo = #{k': end(k') <= a}, hi = #{k': p(k') < e} (< k).  A round is then a
-      // compare against the wave-uniform done mask and the copies: no LDS state besides the bytes.
-      const bool mine = lane < nord;
-      const uint64_t rec = mine ? HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - lane]) : 0ull;
-      const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
-                     dist = (uint32_t)(rec >> 32) & 0xffffu, e = (uint32_t)(rec >> 48);
-      const uint32_t a = p - dist;
-      const uint32_t vp = mine ? p : 0xffffffffu, ve = mine ? p + len : 0xffffffffu;
-      uint32_t lo = 0, hi = 0;
-#pragma unroll
-      for (uint32_t step = 32; step; step >>= 1) {
-        if (__shfl(ve, lo + step - 1u) <= a) lo += step;
-        if (__shfl(vp, hi + step - 1u) < e) hi += step;
-      }
-      const uint64_t need = (hi > lo && mine) ? ((hi - lo == 64u ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo) : 0ull;
-      uint64_t done = ~__ballot(mine);
-      bool fin = !mine;
-      for (;;) {
-        const bool ready = !fin && (done & need) == need;
-        if (ready) rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
-        rs_lds_order();
-        fin = fin || ready;
-        const uint64_t rb = __ballot(ready);
-        done |= rb;
-        if (!__any(!fin)) break;
-        if (rb == 0ull) {  // validated descriptors always make progress: corrupt
-          if (lane == 0) status[b] = INF_DATA;
-          return;
-        }
-      }
-    } else
-#endif
-    if (nord) {
-      for (uint32_t w = lane; w < RS_PW; w += 64) s_pend[w] = 0u;
-      rs_wave_sync();
-      // this lane's matches lane + 64 t: the first in registers (most stretches have fewer
-      // than 64 ordered matches), the rest read back from s_rec each round (registers for six
-      // slots would cost the kernel half its occupancy)
-      const uint32_t mine = nord > lane ? (nord - lane + 63u) / 64u : 0u;
-      uint32_t live = mine >= 32u ? ~0u : (1u << mine) - 1u;
-      const uint64_t rec0 = mine ? HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - lane]) : 0ull;
-      if (mine) rs_bits(s_pend, ((uint32_t)rec0 & 0xffffu) - s0, (uint32_t)(rec0 >> 16) & 0xffffu, true);
-#pragma unroll 1
-      for (uint32_t t = 1; t < mine; ++t) {
-        const uint64_t rec = HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - (lane + 64u * t)]);
-        rs_bits(s_pend, ((uint32_t)rec & 0xffffu) - s0, (uint32_t)(rec >> 16) & 0xffffu, true);
-      }
-      rs_lds_order();
-      auto is_ready = [&](uint64_t rec) {
-        const uint32_t p = (uint32_t)rec & 0xffffu, dist = (uint32_t)(rec >> 32) & 0xffffu;
-        const uint32_t e = (uint32_t)(rec >> 48);
-        const uint32_t a = p - dist;
-        const uint32_t lo = a > s0 ? a - s0 : 0u;  // bytes before the stretch are final
-        return e <= s0 + lo || !rs_any_bit(s_pend, lo, e - s0);
-      };
-      auto run = [&](uint64_t rec) {
-        const uint32_t p = (uint32_t)rec & 0xffffu, len = (uint32_t)(rec >> 16) & 0xffffu,
-                       dist = (uint32_t)(rec >> 32) & 0xffffu;
-        rs_copy_lds(s_buf, lbase + p, len, dist, s_sel);
-        rs_bits(s_pend, p - s0, len, false);
-      };
-      for (;;) {
-        uint32_t ready = (live & 1u) && is_ready(rec0) ? 1u : 0u;
-#pragma unroll 1
-        for (uint32_t t = 1; t < mine; ++t)
-          if ((live >> t & 1u) && is_ready(HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - (lane + 64u * t)]))) ready |= 1u << t;
-        rs_lds_order();
-        if (ready & 1u) run(rec0);
-#pragma unroll 1
-        for (uint32_t t = 1; t < mine; ++t)
-          if (ready >> t & 1u) run(HBAM_RS_UNPACK_ORD(s_rec[RS_MAXM - 1 - (lane + 64u * t)]));
-        live &= ~ready;
-#ifdef HBAM_PROF
-        ++n_bat;
-#endif
-        if (!__any(live != 0u)) break;
-        if (!__any(ready != 0u)) {  // validated descriptors always make progress: corrupt
-          if (lane == 0) status[b] = INF_DATA;
-          return;
-        }
-        rs_lds_order();
-      }
-    }
-    if ((tail0 & 0x80000000u) && (tail0 & 0xffffu) / RS_S == k && lane == 0) {
-      // final match shorter than 3 bytes (the output filled up inside it); last token
-      const uint32_t p = tail0 & 0xffffu, n = (tail0 >> 16) & 0x7fffu;
-      uint32_t d = tails[2 * (uint64_t)b + 1];
-      if (d == 0u || d > p || p + n > isize) {  // corrupt tail token: no copy from outside
-        status[b] = INF_DATA;
-        d = 1u;
-        tail_bad = true;
-      }
-      uint32_t jj = 0;
-      for (uint32_t t = 0; t < n && !tail_bad; ++t) {
-        const uint32_t x = p - d + jj;
-        s_buf[lbase + p + t] = (x + RS_W + a0 >= s0) ? s_buf[lbase + x] : ubuf[base + x];
-        jj = (jj + 1u == d) ? 0u : jj + 1u;
-      }
-    }
-    __syncthreads();
-#ifdef HBAM_PROF
-    const uint64_t q2 = PROF_CLK();
-    p_bat += q2 - q1;
-#endif
-    // ---- write back stretch k (LDS [RS_W, RS_W + RS_S)), then slide the window by RS_S
-    // (each lane moves its own 16-byte columns, so no barrier is needed inside the move).
-    // The stretch is read into registers first and stored to ubuf after the prefetched raw
-    // stretch has been placed and the next one requested: the wait for that prefetch
-    // (vmcnt, which counts stores too) then never waits for this stretch's write-back.
-    uint4 wbv[RS_C];
-#pragma unroll
-    for (uint32_t h = 0; h < RS_C; ++h) wbv[h] = *(const uint4*)(s_buf + RS_W + 1024u * h + 16u * lane);
-    // move [RS_S, RS_S + RS_W + RS_S) down to 0 in 16-byte columns; one wave, so every read of
-    // a 1 KiB step lands before that step's writes (any RS_W that is a multiple of 16)
-#pragma unroll
-    for (uint32_t o = 16u * lane; o < RS_W + RS_S; o += 1024u)
-      *(uint4*)(s_buf + o) = *(const uint4*)(s_buf + RS_S + o);
-    *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = ra0;
-    if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = ra1;
-    load_raw(k + 3, ra0, ra1);
-#pragma unroll
-    for (uint32_t h = 0; h < RS_C; ++h) rs_write_back(ubuf, abase + s0 + 1024u * h + 16u * lane, base, aend, wbv[h]);
-    __syncthreads();
-#ifdef HBAM_PROF
-    p_wb += PROF_CLK() - q2;
-#endif
-  }
-#ifdef HBAM_PROF
-  if (g_prof && lane == 0) {
-    unsigned long long* g = g_prof + 32 * (uint64_t)b;
-    g[0] = pr0;
-    g[1] = PROF_RT();
-    g[2] = PROF_CLK() - pc0;
-    g[3] = p_st;
-    g[4] = p_desc;
-    g[5] = p_bat;
-    g[12] = p_pre;
-    g[13] = p_wb;
-    g[6] = n_bat;
-    g[7] = n_m;
-  }
-#endif
-}
-
+// LZ77 resolution of one block (phase 2 of the batched inflate): k_resolve_units
 #include "resolve_units.h"
-#ifndef HBAM_RS_UNITS
-#define HBAM_RS_UNITS 0  // LZ77 pass: k_resolve_units (16-byte units, aligned masked writes) instead of k_resolve
-#endif
 
 // CRC-32 (IEEE, reflected 0xEDB88320) of each inflated block, slice-by-4 tables in LDS.
 __global__ __launch_bounds__(256) void k_crc32(const BlockRec* __restrict__ blk,

@@ -1,12 +1,12 @@
 // resolve_units.h — LZ77 resolution by 16-byte units (k_resolve_units), gfx950.
 //
-// Same input, output and error contract as k_resolve (resolve_dev.h, hbam_kernels.hip): one wave
-// per BGZF block walks the block in RS_S-byte stretches staged in LDS with an RS_W-byte window
-// behind.  What differs is the unit of work.  k_resolve copies a whole match per lane, so a
-// wave-step runs the union of every lane's copy loop (period < 8, 32-byte groups, 8-byte chunks)
-// and every partial write is a misaligned ds_write_b64/b32/b16/b8 behind its own branch: the LDS
-// pipe spends ~27 % of its cycles in misaligned-access replays and the exec-mask bookkeeping is as
-// many scalar instructions as there are vector ones (round-4 SQ counters).
+// Input / output / error contract: resolve_dev.h.  One wave per BGZF block walks the block in
+// RS_S-byte stretches staged in LDS with an RS_W-byte window behind.  The round-4 kernel (k_resolve,
+// commit 88cff91) copied a whole match per lane, so a wave-step ran the union of every lane's copy
+// loop (period < 8, 32-byte groups, 8-byte chunks) and every partial write was a misaligned
+// ds_write_b64/b32/b16/b8 behind its own branch: the LDS pipe spent ~27 % of its cycles in
+// misaligned-access replays and the exec-mask bookkeeping was as many scalar instructions as there
+// were vector ones (round-4 SQ counters).
 //
 // Here every match is cut, when its descriptor is read, into units of at most 16 bytes whose
 // source never overlaps their own destination:
@@ -37,7 +37,11 @@ __device__ __forceinline__ uint32_t ru_pack(uint32_t rel, uint32_t n, uint32_t d
 
 // 16 bytes at LDS byte index x, from a dword-aligned b128 + b32 (full rate) and v_alignbit
 __device__ __forceinline__ uint4 ru_rd16(const uint8_t* buf, uint32_t x) {
-  const uint32_t a = x & ~3u, sh = (x & 3u) * 8u;
+  uint32_t a = x & ~3u;
+  const uint32_t sh = (x & 3u) * 8u;
+  // hide the 4-byte alignment from the compiler, which would otherwise split the read into a
+  // misaligned ds_read_b64 + ds_read2_b32: one ds_read_b128 at dword alignment runs at full rate
+  asm("" : "+v"(a));
   const uint4 q = *(const uint4*)(buf + a);
   const uint32_t q4 = *(const uint32_t*)(buf + a + 16u);
   return make_uint4(__builtin_amdgcn_alignbit(q.y, q.x, sh), __builtin_amdgcn_alignbit(q.z, q.y, sh),
@@ -103,9 +107,6 @@ __device__ __forceinline__ void ru_copy(uint8_t* __restrict__ buf, uint32_t di, 
   ru_put(buf, di, n, v);
 }
 
-#ifndef HBAM_RU_SEARCH
-#define HBAM_RU_SEARCH 0  // ordered-unit dependency ranks: 0 binary search (ds_bpermute), 1 v_readlane walk
-#endif
 #ifndef HBAM_RU_WAVES
 #define HBAM_RU_WAVES 8
 #endif
@@ -163,10 +164,10 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
   if (RS_C == 2) *(uint4*)(s_buf + RS_W + 1024 + 16u * lane) = ra1;
   *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = rb0;
   if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = rb1;
-  load_raw(2, ra0, ra1);
   constexpr uint32_t WPS = RS_S / 32;
-  uint32_t wnext = (lane < WPS && lane < nwords) ? bm[lane] : 0u;
+  uint32_t wcur = (lane < WPS && lane < nwords) ? bm[lane] : 0u;
   __syncthreads();
+  asm volatile("" : "+v"(wcur));  // defined here for the compiler's wait tracking (see the drain below)
 #ifdef HBAM_PROF
   p_st = PROF_CLK() - pc0;
 #endif
@@ -175,11 +176,9 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
 #ifdef HBAM_PROF
     const uint64_t q0 = PROF_CLK();
 #endif
-    const uint32_t word = wnext;
-    {
-      const uint32_t wi = (k + 1) * WPS + lane;
-      wnext = (lane < WPS && k + 1 < nstr && wi < nwords) ? bm[wi] : 0u;
-    }
+    // this stretch's bitmap words: requested before the previous stretch's drain and in registers
+    // since (a load issued here would make the compiler wait for every store of the last write-back)
+    const uint32_t word = wcur;
     const uint32_t lbase = RS_W + a0 - s0;  // LDS index of block offset x: x + lbase
     // ---- match starts of the stretch -> s_pos (in order)
     const uint32_t cnt = __popc(word);
@@ -213,7 +212,8 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
           D = dist;
         } else if (dist < 8u) {
           h = len < 16u ? len : 16u;
-          D = dist * ((15u + dist) / dist);
+          // dist * ceil(16 / dist) for dist 1..7 = 16 + {0,0,0,2,0,4,2,5}[dist] (no integer division)
+          D = 16u + ((0xAA0400u >> (3u * dist)) & 7u);
           per = true;
         } else {
           h = dist;
@@ -249,22 +249,37 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
     p_desc += q1 - q0;
     n_m += total;
 #endif
-    // ---- pre units: every source final (LDS window, or ubuf written back at least one
-    // iteration ago: the drain below)
-    if (s0 >= RS_W) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (uint32_t i = lane; i < npre; i += 64) {
-      const uint32_t r = s_unit[i];
-      const uint32_t q = s0 + (r & 2047u), n = ((r >> 11) & 15u) + 1u, dist = ((r >> 15) & 0x7fffu) + 1u;
-      const uint32_t src = q - dist;
-      uint4 v;
-      if (src + RS_W + a0 >= s0) {
-        v = ru_rd16(s_buf, lbase + src);
-      } else {  // older than the window: dist > RS_W, the unit ends before the stretch
-        v = *(const uint4*)(ubuf + base + src);
+    // ---- pre units: every source final (the LDS window, or ubuf written back at least one
+    // iteration ago, which the drain makes visible).  The next stretch's bitmap words are
+    // requested first, so they land with the drain.
+    {
+      const uint32_t wi = (k + 1) * WPS + lane;
+      wcur = (lane < WPS && k + 1 < nstr && wi < nwords) ? bm[wi] : 0u;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" : "+v"(wcur));  // the next stretch's words land with the drain
+    // two units per lane per step, both sources requested before either is written: the far
+    // (global) reads of a step are in flight together
+    for (uint32_t i = lane; i < npre; i += 128) {
+      const bool two = i + 64u < npre;
+      const uint32_t r = s_unit[i], r2 = two ? s_unit[i + 64u] : 0u;
+      const uint32_t q = s0 + (r & 2047u), dist = ((r >> 15) & 0x7fffu) + 1u;
+      const uint32_t q2 = s0 + (r2 & 2047u), dist2 = ((r2 >> 15) & 0x7fffu) + 1u;
+      const uint32_t src = q - dist, src2 = q2 - dist2;
+      uint4 v, v2 = make_uint4(0, 0, 0, 0);
+      if (src + RS_W + a0 >= s0) v = ru_rd16(s_buf, lbase + src);
+      else v = *(const uint4*)(ubuf + base + src);
+      if (two) {
+        if (src2 + RS_W + a0 >= s0) v2 = ru_rd16(s_buf, lbase + src2);
+        else v2 = *(const uint4*)(ubuf + base + src2);
       }
-      ru_put(s_buf, lbase + q, n, v);
+      ru_put(s_buf, lbase + q, ((r >> 11) & 15u) + 1u, v);
+      if (two) ru_put(s_buf, lbase + q2, ((r2 >> 11) & 15u) + 1u, v2);
     }
     rs_lds_order();
+    // raw stretch k+2 requested only now: the far reads above never wait behind it in vmcnt
+    // order, and the ordered rounds below (no global access) cover its latency
+    load_raw(k + 2, ra0, ra1);
 #ifdef HBAM_PROF
     p_pre += PROF_CLK() - q1;
 #endif
@@ -280,19 +295,11 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
       const uint32_t a = q - dist, e = per ? q : a + n;
       const uint32_t vp = mine ? q : 0xffffffffu, ve = mine ? q + n : 0xffffffffu;
       uint32_t lo = 0, hi = 0;
-#if HBAM_RU_SEARCH
-      // ranks by a uniform walk over the units (v_readlane: no LDS), units sorted by destination
-      for (uint32_t v = 0; v < nord; ++v) {
-        lo += (uint32_t)__builtin_amdgcn_readlane((int)ve, (int)v) <= a ? 1u : 0u;
-        hi += (uint32_t)__builtin_amdgcn_readlane((int)vp, (int)v) < e ? 1u : 0u;
-      }
-#else
 #pragma unroll
       for (uint32_t step = 32; step; step >>= 1) {
         if (__shfl(ve, lo + step - 1u) <= a) lo += step;
         if (__shfl(vp, hi + step - 1u) < e) hi += step;
       }
-#endif
       const uint64_t need = (hi > lo && mine) ? ((hi - lo == 64u ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo) : 0ull;
       uint64_t done = ~__ballot(mine);
       bool fin = !mine;
@@ -383,7 +390,6 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
     for (uint32_t o = 16u * lane; o < RS_W + RS_S; o += 1024u) *(uint4*)(s_buf + o) = *(const uint4*)(s_buf + RS_S + o);
     *(uint4*)(s_buf + RS_W + RS_S + 16u * lane) = ra0;
     if (RS_C == 2) *(uint4*)(s_buf + RS_W + RS_S + 1024 + 16u * lane) = ra1;
-    load_raw(k + 3, ra0, ra1);
 #pragma unroll
     for (uint32_t h2 = 0; h2 < RS_C; ++h2) rs_write_back(ubuf, abase + s0 + 1024u * h2 + 16u * lane, base, aend, wbv[h2]);
     __syncthreads();
