@@ -186,6 +186,9 @@ enum BufId {
 #define HBAM_INFLATE_SLICES 1  // A/B at 10 GB: 1 -> 163.4 ms, 2 -> 161.5, 4 -> 166.5, 8 -> 164.5 (Huffman + LZ77)
 #endif
 #define HBAM_MAX_SLICES 16
+#ifndef HBAM_POOLS2
+#define HBAM_POOLS2 0  // pools kernel: k_decode_pools2 (DPP scans, LDS record table) instead of k_decode_pools
+#endif
 #ifndef HBAM_WAVE_MAX_BLOCKS
 // Huffman pass by k_inflate_wave (a wave per block) for calls of up to this many BGZF blocks,
 // by k_inflate_tokens (a lane per block) above: the lane pass needs ~131k blocks (2 waves x 64
@@ -504,7 +507,7 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
   if ((rc = ensure(c, B_EDGE, 32 * nb + 32, &edges))) return rc;
   uint32_t* retry = nullptr;  // [HBAM_MAX_SLICES counters][nb block indices]
-  const bool wave = HBAM_INFLATE_WAVE && nb <= c->wave_max_blocks;
+  const bool wave = nb <= c->wave_max_blocks;
   if (wave) {
     if ((rc = ensure(c, B_RETRY, nb + HBAM_MAX_SLICES, &retry))) return rc;
     HIPCHK(c, hipMemsetAsync(retry, 0, HBAM_MAX_SLICES * 4, c->stream));
@@ -552,7 +555,6 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
     }
   }
   HIPCHK(c, hipGetLastError());
-#if HBAM_INFLATE_WAVE
   if (wave && nb && getenv("HBAM_WV_STATS")) {  // diagnostics: blocks the wave pass left to the lane pass
     uint32_t cnt[HBAM_MAX_SLICES];
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -571,7 +573,6 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
     HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(g_wvprof), z, sizeof(z)));
 #endif
   }
-#endif
   if (want_crc && nb) {
     k_crc32<<<grid_for(nb, 256), 256, 0, c->stream>>>(blk, uoff, (uint32_t)nb, ubuf, crc);
     HIPCHK(c, hipGetLastError());
@@ -1210,8 +1211,13 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if ((rc = ensure(c, B_C_AUX, tot_aux + 1, &dc.aux))) return rc;
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   if (n_final)
+#if HBAM_POOLS2
+    k_decode_pools2<<<(uint32_t)std::min<uint64_t>(grid_for(n_final, 256), POOLS_MAX_WG), 256, 0, c->stream>>>(
+        ub, n_final, rec_off, dc);
+#else
     k_decode_pools<<<(uint32_t)std::min<uint64_t>(grid_for(n_final, 256), POOLS_MAX_WG), 256, 0, c->stream>>>(
         ub, n_final, rec_off, dc);
+#endif
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2196,14 +2202,9 @@ extern "C" int hbam_gather_records(hbam_ctx* c, const uint8_t* ubuf, const uint6
   if (n) {
     // one wave per record, grid-stride: a grid of 64 x n threads would pass 2^32 above 67 M
     // records (the dispatch packet's grid size is 32-bit)
-#if HBAM_GATHER_TILE
     // a wave per 64-record tile (A/B against the wave-per-record gather: profiles/r04/ab/)
     k_gather_records_tile<<<(uint32_t)std::min<uint64_t>((n + 255) / 256, POOLS_MAX_WG), 256, 0, c->stream>>>(
         ubuf, rec_off, perm, n, out_off, out);
-#else
-    const uint64_t g = std::min<uint64_t>((n + RS_WG / 64 - 1) / (RS_WG / 64), GATHER_MAX_WG);
-    k_gather_records<<<(uint32_t)g, RS_WG, 0, c->stream>>>(ubuf, rec_off, perm, n, out_off, out);
-#endif
   }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev[10], c->stream));

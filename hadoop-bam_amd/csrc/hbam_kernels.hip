@@ -307,9 +307,6 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
 #endif
 }
 
-#ifndef HBAM_INFLATE_WAVE
-#define HBAM_INFLATE_WAVE 1  // Huffman pass: wave per block (inflate_wave.h) with the lane-per-block pass for the rest
-#endif
 // Huffman pass, one wave (= one workgroup) per BGZF block; see inflate_wave.h.  Blocks it does
 // not take are appended to list for k_inflate_tokens.
 __global__ __launch_bounds__(64, HBAM_WV_WAVES) void k_inflate_wave(const uint8_t* __restrict__ comp,
@@ -918,6 +915,87 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
           const u32x4_a1 v = f == 2 ? seq16(u + sq + 8u * k) : *(const u32x4_a1*)(u + sq + 16u * k);
           // (the pieces of the last unit cost 0.5 of 8.3 ms at 5 GB against full 16-byte stores:
           // profiles/r03/ab/pools_tail_cost_5g.txt)
+          if (n >= 16u) *(u32x4_a1*)dp = v;
+          else st_part(dp, n, v);
+        }
+      }
+    }
+  }
+}
+
+// The same pools with the unit -> record mapping done without the LDS pipe's shuffles: k_decode_pools
+// spends ~11 ds_bpermute per 64 units (a 6-step binary search over the lanes' first units plus
+// the record's fields) and 7 per field scan.  Here the scans are DPP, each record with units
+// writes (source, destination, bytes, first unit) once into LDS at its rank among the tile's
+// records with units, and a unit finds its record's rank as a popcount: the records whose first
+// unit lies in the 64-unit window are one bit each of a mask (distinct positions), the earlier
+// ones are counted by one ballot.  One ds_read_b128 per unit instead of eleven dependent shuffles.
+static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l) << 32;
+}
+__global__ __launch_bounds__(256) void k_decode_pools2(const uint8_t* __restrict__ u, uint64_t nrec,
+                                                       const uint64_t* __restrict__ rec_off,
+                                                       DevColumns c) {
+  __shared__ uint4 s_recs[4][64];
+  const uint32_t lane = threadIdx.x & 63u;
+  uint4* const recs = s_recs[threadIdx.x >> 6];
+  const uint64_t ntiles = (nrec + 63) / 64;
+  const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
+  const uint64_t le = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= this one
+  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); t < ntiles; t += wstride) {
+    const uint64_t r = t * 64 + lane;
+    uint32_t nl = 0, nc = 0, ls = 0, na = 0;
+    uint64_t src = 0, o_name = 0, o_cig = 0, o_seq = 0, o_aux = 0;
+    if (r < nrec && c.layout_ok[r]) {
+      src = rec_off[r] + 36;
+      nl = c.name_len[r];
+      nc = c.cigar_n[r];
+      ls = c.seq_len[r];
+      na = c.aux_len[r];
+      o_name = c.name_off[r];
+      o_cig = c.cigar_off[r];
+      o_seq = c.seq_off[r];
+      o_aux = c.aux_off[r];
+    }
+#pragma unroll 1
+    for (uint32_t f = 0; f < 5; ++f) {
+      uint32_t len;
+      uint64_t s0, d0;
+      uint8_t* base;
+      if (f == 0) { len = nl; s0 = src; d0 = o_name; base = c.names; }
+      else if (f == 1) { len = 4u * nc; s0 = src + nl; d0 = 4 * o_cig; base = (uint8_t*)c.cigars; }
+      else if (f == 2) { len = ls; s0 = src + nl + 4u * nc; d0 = o_seq; base = c.seq; }
+      else if (f == 3) { len = ls; s0 = src + nl + 4u * nc + (ls + 1u) / 2u; d0 = o_seq; base = c.qual; }
+      else { len = na; s0 = src + nl + 4u * nc + (ls + 1u) / 2u + ls; d0 = o_aux; base = c.aux; }
+      const uint32_t units = (len + 15u) >> 4;
+      const uint32_t incl = wave_scan_dpp(units), excl = incl - units, total = wave_last(incl);
+      if (total == 0u) continue;
+      const bool has = units != 0u;
+      const uint64_t mh = __ballot(has);
+      const uint32_t first = (uint32_t)__builtin_ctzll(mh);
+      const uint64_t sb = readlane64(s0, first), db = readlane64(d0, first);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");  // the previous field's reads of recs precede these writes
+      if (has) recs[lane_rank(mh)] = make_uint4((uint32_t)(s0 - sb), (uint32_t)(d0 - db), len, excl);
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");  // (one wave: its LDS operations run in issue order)
+      uint8_t* const dbase = base + db;
+      const uint8_t* const sbase = u + sb;
+      for (uint32_t q0 = 0; q0 < total; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        // the window's record starts, one bit each, and the records that start before it
+        const uint32_t pos = excl - q0;
+        const bool inwin = has && excl >= q0 && pos < 64u;
+        const uint32_t blo = (inwin && pos < 32u) ? 1u << pos : 0u;
+        const uint32_t bhi = (inwin && pos >= 32u) ? 1u << (pos - 32u) : 0u;
+        const uint64_t M = (uint64_t)wave_last(wave_scan_dpp(bhi)) << 32 | wave_last(wave_scan_dpp(blo));
+        const uint32_t c0 = (uint32_t)__popcll(__ballot(has && excl < q0));
+        if (q < total) {
+          const uint4 rr = recs[c0 + (uint32_t)__popcll(M & le) - 1u];
+          const uint32_t k = q - rr.w, n = rr.z - 16u * k;
+          uint8_t* dp = dbase + rr.y + 16u * k;
+          const u32x4_a1 v = f == 2 ? seq16(sbase + rr.x + 8u * k) : *(const u32x4_a1*)(sbase + rr.x + 16u * k);
           if (n >= 16u) *(u32x4_a1*)dp = v;
           else st_part(dp, n, v);
         }

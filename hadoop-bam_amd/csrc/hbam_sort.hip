@@ -137,42 +137,8 @@ __global__ __launch_bounds__(RS_WG) void k_perm_lens(const int32_t* __restrict__
   if (i < n) lens[i] = 4u + (uint32_t)block_size[perm ? perm[i] : i];
 }
 
-// one wave per record: copy 4 + block_size bytes from ubuf[rec_off[perm[i]]] to out[out_off[i]]
-__global__ __launch_bounds__(RS_WG) void k_gather_records(const uint8_t* __restrict__ ubuf,
-                                                          const uint64_t* __restrict__ rec_off,
-                                                          const uint32_t* __restrict__ perm,
-                                                          uint64_t n,
-                                                          const uint64_t* __restrict__ out_off,
-                                                          uint8_t* __restrict__ out) {
-  const uint32_t lane = threadIdx.x & 63u;
-  for (uint64_t i = (uint64_t)blockIdx.x * (RS_WG / 64) + (threadIdx.x >> 6); i < n;
-       i += (uint64_t)gridDim.x * (RS_WG / 64)) {
-    const uint64_t src = rec_off[perm ? perm[i] : i];
-    const uint64_t dst = out_off[i];
-    const uint32_t len = (uint32_t)(out_off[i + 1] - dst);
-    const uint8_t* s = ubuf + src;
-    uint8_t* d = out + dst;
-    if (((src ^ dst) & 3u) == 0) {
-      // co-aligned: bytes up to the first dword boundary, dwords, then the tail
-      const uint32_t head = (uint32_t)((4u - (dst & 3u)) & 3u) < len ? (uint32_t)((4u - (dst & 3u)) & 3u) : len;
-      if (lane < head) d[lane] = s[lane];
-      const uint32_t nw = (len - head) >> 2;
-      const uint32_t* s4 = (const uint32_t*)(s + head);
-      uint32_t* d4 = (uint32_t*)(d + head);
-      for (uint32_t k = lane; k < nw; k += 64) d4[k] = s4[k];
-      const uint32_t t0 = head + 4u * nw;
-      if (t0 + lane < len) d[t0 + lane] = s[t0 + lane];
-    } else {
-      for (uint32_t k = lane; k < len; k += 64) d[k] = s[k];
-    }
-  }
-}
-
-#ifndef HBAM_GATHER_TILE
-#define HBAM_GATHER_TILE 1
-#endif
-#if HBAM_GATHER_TILE
-// The same gather, a wave per tile of 64 consecutive output records (k_decode_pools' unit
+// The record gather (SAMRecordWritable payloads in permutation order), a wave per tile of 64
+// consecutive output records (k_decode_pools' unit
 // scheme): each lane reads its record's source offset and length once, every record is cut into
 // 16-byte units numbered by a wave scan, and consecutive lanes take consecutive units (a unit's
 // record found by a 6-step shuffle search), so a wave instruction moves ~1 KiB of the output
@@ -237,7 +203,6 @@ __global__ __launch_bounds__(256) void k_gather_records_tile(const uint8_t* __re
     }
   }
 }
-#endif
 
 // TotalOrderPartitioner bounds: for split point j, the first index whose (signed) key is
 // greater (partition j holds keys <= sp[j]); sorted keys, one thread per split point

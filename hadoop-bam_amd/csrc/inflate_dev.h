@@ -31,42 +31,21 @@ enum : int32_t {
   INF_DATA = 2,   // zlib Z_DATA_ERROR (DataFormatException)
 };
 
-// Cache-policy switches for the batched inflate's streams (A/B builds: -DHBAM_NT_LOAD=1 /
-// -DHBAM_NT_STORE=1 mark the per-lane compressed-input loads / token-output stores
-// non-temporal so they do not evict each other's lines from the 4 MiB per-XCD L2).
-#ifndef HBAM_NT_LOAD
-#define HBAM_NT_LOAD 0
-#endif
-#ifndef HBAM_NT_STORE
-// Off: non-temporal token stores cut the Huffman pass's input FETCH to C (6.1 -> 2.1 GB per
-// 2 GB decode), but their write acknowledgements are slow and every epoch's `s_waitcnt vmcnt(0)`
-// (vmcnt counts stores too on CDNA) waits for the last iteration's stores: 105 -> 70 ms at
-// 10 GB with plain stores (profiles/r02/s2/ab_store_epoch_10g.txt).
-#define HBAM_NT_STORE 0
-#endif
+// The batched inflate's input loads and token stores use the default cache policy.  Measured and
+// dropped (round 2): non-temporal token stores cut the Huffman pass's input FETCH to C (6.1 ->
+// 2.1 GB per 2 GB decode), but their write acknowledgements are slow and every epoch's
+// `s_waitcnt vmcnt(0)` (vmcnt counts stores too on CDNA) waits for the last iteration's stores:
+// 105 -> 70 ms at 10 GB with plain stores (profiles/r02/s2/ab_store_epoch_10g.txt); non-temporal
+// input loads 69.9 vs 70 ms.
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_quad(const uint4* p) {
-#if HBAM_NT_LOAD
-  const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
-  return make_uint4(v.x, v.y, v.z, v.w);
-#else
   return *p;
-#endif
 }
 __device__ __forceinline__ void st_out(uint4* p, uint4 v) {
-#if HBAM_NT_STORE
-  u32x4_t w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, (u32x4_t*)p);
-#else
   *p = v;
-#endif
 }
 __device__ __forceinline__ void st_out(uint32_t* p, uint32_t v) {
-#if HBAM_NT_STORE
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
 }
 
 struct BitIn {

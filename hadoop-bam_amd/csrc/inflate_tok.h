@@ -49,9 +49,6 @@ namespace hbam {
 #endif
 constexpr uint32_t TOK_K = HBAM_TOK_K;
 
-#ifndef HBAM_TOK_DOT2
-#define HBAM_TOK_DOT2 1  // dot2 accumulation in the packed lookup: 68.5 -> 67.5 ms at 10 GB (profiles/r02/s2/ab_dot2_10g.txt)
-#endif
 // The fast path (tok_fast_spec): up to two literals and a match per iteration, decoded first
 // (both lit/len lookups before either LDS symbol read), then written as one packet
 // (TSink::put): 66.4 -> 60.3 ms at 10 GB against the same decode with one sink call per token
@@ -199,7 +196,6 @@ __device__ __forceinline__ void huffp_make(const Huff& h, HuffP& p) {
 // each cost a hazard s_nop):
 //   g  = min(sat(v+1 - lim_j), 1)   the two "v >= lim" bits as 0/1 halves
 //   sl += g;  so += g * dof_j;  st += g * dhl_j
-#if HBAM_TOK_DOT2
 // v_dot2_u32_u16 folds both halves into one u32 accumulator per pair, so the sums need no
 // final (x & 0xffff) + (x >> 16) step (offsets stay exact mod 2^16: results are masked)
 #define HBAM_PK_PAIR(LIM, DOF, DHL)                 \
@@ -213,19 +209,6 @@ __device__ __forceinline__ void huffp_make(const Huff& h, HuffP& p) {
   "v_pk_min_u16 %[g], %[g], %[one]\n\t"              \
   "v_dot2_u32_u16 %[sl], %[g], %[one], %[sl]\n\t"    \
   "v_dot2_u32_u16 %[so], %[g], " DOF ", %[so]\n\t"
-#else
-#define HBAM_PK_PAIR(LIM, DOF, DHL)                 \
-  "v_pk_sub_u16 %[g], %[vv], " LIM " clamp\n\t"     \
-  "v_pk_min_u16 %[g], %[g], %[one]\n\t"              \
-  "v_pk_add_u16 %[sl], %[sl], %[g]\n\t"              \
-  "v_pk_mad_u16 %[so], %[g], " DOF ", %[so]\n\t"     \
-  "v_pk_mad_u16 %[st], %[g], " DHL ", %[st]\n\t"
-#define HBAM_PK_PAIR_NT(LIM, DOF)                   \
-  "v_pk_sub_u16 %[g], %[vv], " LIM " clamp\n\t"     \
-  "v_pk_min_u16 %[g], %[g], %[one]\n\t"              \
-  "v_pk_add_u16 %[sl], %[sl], %[g]\n\t"              \
-  "v_pk_mad_u16 %[so], %[g], " DOF ", %[so]\n\t"
-#endif
 template <bool HI>
 __device__ __forceinline__ bool huffp_lookup(const HuffP& h, uint32_t v, uint32_t& L, uint32_t& idx,
                                              uint32_t& hi) {
@@ -257,17 +240,10 @@ __device__ __forceinline__ bool huffp_lookup(const HuffP& h, uint32_t v, uint32_
           [d0] "v"(h.dof[0]), [d1] "v"(h.dof[1]), [d2] "v"(h.dof[2]), [d3] "v"(h.dof[3]),
           [d4] "v"(h.dof[4]), [d5] "v"(h.dof[5]), [d6] "v"(h.dof[6]));
   }
-#if HBAM_TOK_DOT2
   const uint32_t l = 1u + sl;
   L = l;
   idx = (h.o0 + so + (v >> (15u - l))) & 0xffffu;
   if (HI) hi = v >= ((h.t0 + st) & 0xffffu) ? 256u : 0u;
-#else
-  const uint32_t l = 1u + (sl & 0xffffu) + (sl >> 16);
-  L = l;
-  idx = (h.o0 + so + (so >> 16) + (v >> (15u - l))) & 0xffffu;
-  if (HI) hi = v >= ((h.t0 + st + (st >> 16)) & 0xffffu) ? 256u : 0u;
-#endif
   return v < h.lim14;
 }
 

@@ -334,15 +334,8 @@ __device__ bool wv_header(WvLds& S, WvHdr& h, uint32_t& q, uint32_t E, bool& bfi
 // do-while loops with a scalar epoch branch, as the lane pass's symbol loop (a wave-uniform
 // `while (__any(...))` loop made the compiler copy the reader's registers, and wait on the quad in
 // flight, at every iteration).
-#ifndef HBAM_WV_NT
-#define HBAM_WV_NT 0  // non-temporal input quads (A/B)
-#endif
 __device__ __forceinline__ u32x4_t wv_load(const uint4* p) {
-#if HBAM_WV_NT
-  return __builtin_nontemporal_load((const u32x4_t*)p);
-#else
   return ein_load(p);
-#endif
 }
 struct WvBits {
   uint64_t bb;

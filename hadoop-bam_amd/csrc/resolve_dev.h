@@ -100,6 +100,19 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
   return x;
 }
 
+// inclusive wave scan (+) with DPP row shifts and row broadcasts (GFX9 DPP): no LDS traffic, where
+// a __shfl_up scan is six ds_bpermute_b32 through the LDS pipe
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_last(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
+
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits below this lane
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));

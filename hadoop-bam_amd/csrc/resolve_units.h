@@ -48,19 +48,6 @@ __device__ __forceinline__ uint4 ru_rd16(const uint8_t* buf, uint32_t x) {
                     __builtin_amdgcn_alignbit(q.w, q.z, sh), __builtin_amdgcn_alignbit(q4, q.w, sh));
 }
 
-// inclusive wave scan (+) with DPP row shifts and row broadcasts: no LDS traffic (a __shfl_up
-// scan is six ds_bpermute_b32 through the LDS pipe this kernel is bound by)
-__device__ __forceinline__ uint32_t ru_scan(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return x;
-}
-__device__ __forceinline__ uint32_t ru_last(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
-
 __device__ __forceinline__ uint32_t ru_lowbytes(uint32_t k) {  // mask of the low k (0..4) bytes
   return k >= 4u ? ~0u : (1u << (8u * k)) - 1u;
 }
@@ -182,8 +169,8 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
     const uint32_t lbase = RS_W + a0 - s0;  // LDS index of block offset x: x + lbase
     // ---- match starts of the stretch -> s_pos (in order)
     const uint32_t cnt = __popc(word);
-    const uint32_t incl = ru_scan(cnt);
-    const uint32_t total = ru_last(incl);
+    const uint32_t incl = wave_scan_dpp(cnt);
+    const uint32_t total = wave_last(incl);
     {
       uint32_t wpos = incl - cnt, bits = word;
       while (bits) {
@@ -222,7 +209,7 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
         nu = (h ? 1u : 0u) + (len - h + 15u) / 16u;
       }
       const uint32_t up = pre ? nu : 0u, uo = pre ? 0u : nu;
-      const uint32_t ipo = ru_scan(up | uo << 16);  // both counts in one scan (each < 2^16)
+      const uint32_t ipo = wave_scan_dpp(up | uo << 16);  // both counts in one scan (each < 2^16)
       const uint32_t ip = ipo & 0xffffu, io = ipo >> 16;
       if (up) {
         const uint32_t w = npre + ip - up;
@@ -235,7 +222,7 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
         for (uint32_t q = p + h; u < uo; ++u, q += 16u)
           s_unit[RU_CAP - 1u - (w + u)] = ru_pack(q - s0, p + len - q < 16u ? p + len - q : 16u, D, false);
       }
-      const uint32_t tpo = ru_last(ipo);
+      const uint32_t tpo = wave_last(ipo);
       npre += tpo & 0xffffu;
       nord += tpo >> 16;
     }

@@ -30,16 +30,9 @@ __device__ __forceinline__ bool huffp_lookup(const HuffP& h, uint32_t v, uint32_
       const uint32_t g = (v + 1u > lim) ? 1u : 0u;
       const uint32_t dof = (h.dof[j] >> (16 * q)) & 0xffffu;
       const uint32_t dhl = HI ? ((h.dhl[j] >> (16 * q)) & 0xffffu) : 0u;
-#if HBAM_TOK_DOT2
-      sl += g;
+      sl += g;  // v_dot2_u32_u16 accumulation (both sources: the r02 one with HBAM_TOK_DOT2 = 1)
       so += g * dof;
       if (HI) st += g * dhl;
-#else
-      const uint32_t sh = 16u * (uint32_t)q, m = 0xffffu << sh;
-      sl = (sl & ~m) | ((((sl >> sh) + g) & 0xffffu) << sh);
-      so = (so & ~m) | ((((so >> sh) + g * dof) & 0xffffu) << sh);
-      if (HI) st = (st & ~m) | ((((st >> sh) + g * dhl) & 0xffffu) << sh);
-#endif
     }
   }
 '''
@@ -53,7 +46,10 @@ def transform(src):
     # the lookup: from its template line through the asm blocks up to the shared tail
     head = "template <bool HI>\n__device__ __forceinline__ bool huffp_lookup("
     i = out.index(head)
-    j = out.index("#if HBAM_TOK_DOT2\n  const uint32_t l = 1u + sl;", i)
+    # the shared tail: behind `#if HBAM_TOK_DOT2` in the r02 source, plain since round 5
+    j = out.find("#if HBAM_TOK_DOT2\n  const uint32_t l = 1u + sl;", i)
+    if j < 0:
+        j = out.index("  const uint32_t l = 1u + sl;", i)
     return out[:i] + LOOKUP_C + out[j:]
 
 
