@@ -186,9 +186,6 @@ enum BufId {
 #define HBAM_INFLATE_SLICES 1  // A/B at 10 GB: 1 -> 163.4 ms, 2 -> 161.5, 4 -> 166.5, 8 -> 164.5 (Huffman + LZ77)
 #endif
 #define HBAM_MAX_SLICES 16
-#ifndef HBAM_POOLS2
-#define HBAM_POOLS2 0  // pools kernel: k_decode_pools2 (DPP scans, LDS record table) instead of k_decode_pools
-#endif
 #ifndef HBAM_WAVE_MAX_BLOCKS
 // Huffman pass by k_inflate_wave (a wave per block) for calls of up to this many BGZF blocks,
 // by k_inflate_tokens (a lane per block) above: the lane pass needs ~131k blocks (2 waves x 64
@@ -1211,13 +1208,8 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   if ((rc = ensure(c, B_C_AUX, tot_aux + 1, &dc.aux))) return rc;
   HIPCHK(c, hipEventRecord(c->ev[7], c->stream));
   if (n_final)
-#if HBAM_POOLS2
-    k_decode_pools2<<<(uint32_t)std::min<uint64_t>(grid_for(n_final, 256), POOLS_MAX_WG), 256, 0, c->stream>>>(
-        ub, n_final, rec_off, dc);
-#else
     k_decode_pools<<<(uint32_t)std::min<uint64_t>(grid_for(n_final, 256), POOLS_MAX_WG), 256, 0, c->stream>>>(
         ub, n_final, rec_off, dc);
-#endif
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev[8], c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -852,89 +852,19 @@ static __device__ __forceinline__ u32x4_a1 seq16(const uint8_t* __restrict__ s) 
   for (int j = 0; j < 4; ++j) o[j] = seq4((uint32_t)(q >> (16 * j)) & 0xffu, (uint32_t)(q >> (16 * j + 8)) & 0xffu);
   return o;
 }
-__global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict__ u, uint64_t nrec,
-                                                      const uint64_t* __restrict__ rec_off,
-                                                      DevColumns c) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t ntiles = (nrec + 63) / 64;
-  const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
-  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); t < ntiles; t += wstride) {
-    const uint64_t r = t * 64 + lane;
-    uint32_t nl = 0, nc = 0, ls = 0, na = 0;
-    uint64_t src = 0, o_name = 0, o_cig = 0, o_seq = 0, o_aux = 0;
-    if (r < nrec && c.layout_ok[r]) {
-      src = rec_off[r] + 36;
-      nl = c.name_len[r];
-      nc = c.cigar_n[r];
-      ls = c.seq_len[r];
-      na = c.aux_len[r];
-      o_name = c.name_off[r];
-      o_cig = c.cigar_off[r];
-      o_seq = c.seq_off[r];
-      o_aux = c.aux_off[r];
-    }
-    // field f: 0 names, 1 CIGAR bytes, 2 SEQ characters, 3 QUAL, 4 AUX
-#pragma unroll 1
-    for (uint32_t f = 0; f < 5; ++f) {
-      uint32_t len;
-      uint64_t s0, d0;
-      uint8_t* base;
-      if (f == 0) { len = nl; s0 = src; d0 = o_name; base = c.names; }
-      else if (f == 1) { len = 4u * nc; s0 = src + nl; d0 = 4 * o_cig; base = (uint8_t*)c.cigars; }
-      else if (f == 2) { len = ls; s0 = src + nl + 4u * nc; d0 = o_seq; base = c.seq; }
-      else if (f == 3) { len = ls; s0 = src + nl + 4u * nc + (ls + 1u) / 2u; d0 = o_seq; base = c.qual; }
-      else { len = na; s0 = src + nl + 4u * nc + (ls + 1u) / 2u + ls; d0 = o_aux; base = c.aux; }
-      const uint32_t units = (len + 15u) >> 4;
-      const uint32_t incl = wave_incl_sum(units, lane);
-      const uint32_t excl = incl - units;
-      const uint32_t total = __shfl(incl, 63);
-      // all 64 lanes stay active through the shuffles (a lane past the last unit reads but
-      // does not write): ds_bpermute does not return the value of a lane the exec mask has
-      // switched off (a build with one shuffle under `q < total` corrupted names and AUX).
-      // Not kept (profiles/r03/ab/pools_*_5g.txt, 5 GB): two or four units per lane per step,
-      // loads first, 8.7 / 9.9 vs 8.3 ms; a division in place of the search for tiles whose
-      // records all have the same unit count, 8.4 vs 8.2; software-pipelined by one unit, 8.6
-      // vs 8.5; all five fields' units numbered together in source order (every line of the
-      // record stream fetched once: FETCH 75.5 -> 29.9 GB per 10 GB shard, WRITE 30.6 -> 36.2),
-      // 8.8 vs 8.5 ms.  The kernel is bound by its per-unit latency, not by HBM traffic.
-      for (uint32_t q0 = 0; q0 < total; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        // the record of unit q: the last lane whose first unit is <= q
-        uint32_t lo = 0;
-#pragma unroll
-        for (uint32_t step = 32; step; step >>= 1) {
-          const uint32_t m = lo + step;
-          if (__shfl(excl, m) <= q) lo = m;
-        }
-        const uint32_t k = q - __shfl(excl, lo);      // unit index inside the segment
-        const uint32_t n = __shfl(len, lo) - 16u * k;  // bytes left in the segment
-        const uint64_t sq = __shfl(s0, lo), dq = __shfl(d0, lo);
-        if (q < total) {
-          uint8_t* dp = base + dq + 16u * k;
-          // 16 SEQ characters come from 8 packed bytes; over-reads stay in ubuf + slack
-          const u32x4_a1 v = f == 2 ? seq16(u + sq + 8u * k) : *(const u32x4_a1*)(u + sq + 16u * k);
-          // (the pieces of the last unit cost 0.5 of 8.3 ms at 5 GB against full 16-byte stores:
-          // profiles/r03/ab/pools_tail_cost_5g.txt)
-          if (n >= 16u) *(u32x4_a1*)dp = v;
-          else st_part(dp, n, v);
-        }
-      }
-    }
-  }
-}
-
-// The same pools with the unit -> record mapping done without the LDS pipe's shuffles: k_decode_pools
-// spends ~11 ds_bpermute per 64 units (a 6-step binary search over the lanes' first units plus
-// the record's fields) and 7 per field scan.  Here the scans are DPP, each record with units
-// writes (source, destination, bytes, first unit) once into LDS at its rank among the tile's
-// records with units, and a unit finds its record's rank as a popcount: the records whose first
-// unit lies in the 64-unit window are one bit each of a mask (distinct positions), the earlier
-// ones are counted by one ballot.  One ds_read_b128 per unit instead of eleven dependent shuffles.
+// The unit -> record mapping without the LDS pipe's shuffles (round 5; the round-4 kernel spent
+// ~11 ds_bpermute per 64 units on a 6-step binary search over the lanes' first units plus the
+// record's fields, and 7 per field scan: 9.17 -> 8.87 ms at 5 GB, same pools,
+// profiles/r05/ab/pools2_dpp_table_5g.txt).  The scans are DPP, each record with units writes
+// (source, destination, bytes, first unit) once into LDS at its rank among the tile's records
+// with units, and a unit finds its record's rank as a popcount: the records whose first unit lies
+// in the 64-unit window are one bit each of a mask (distinct positions), the earlier ones are
+// counted by one ballot.  One ds_read_b128 per unit.
 static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
   return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l) << 32;
 }
-__global__ __launch_bounds__(256) void k_decode_pools2(const uint8_t* __restrict__ u, uint64_t nrec,
+__global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict__ u, uint64_t nrec,
                                                        const uint64_t* __restrict__ rec_off,
                                                        DevColumns c) {
   __shared__ uint4 s_recs[4][64];
