@@ -86,16 +86,48 @@ __device__ __forceinline__ uint4 ru_periodic(uint4 v, uint32_t d, const uint4* _
                     __builtin_amdgcn_perm(v.y, v.x, s.z), __builtin_amdgcn_perm(v.y, v.x, s.w));
 }
 
+// the same with all five writes issued (a dword the unit does not reach gets mask 0: D unchanged),
+// so the caller's exec mask needs no per-dword branches
+__device__ __forceinline__ void ru_put5(uint8_t* buf, uint32_t x, uint32_t n, const uint4 v) {
+  const uint32_t o = x & 3u, e = o + n, rs = 32u - 8u * o;
+  const uint32_t addr = (uint32_t)(uintptr_t)(buf + (x & ~3u));
+  const uint32_t d0 = v.x << (8u * o);
+  const uint32_t d1 = (uint32_t)((((uint64_t)v.y << 32) | v.x) >> rs);
+  const uint32_t d2 = (uint32_t)((((uint64_t)v.z << 32) | v.y) >> rs);
+  const uint32_t d3 = (uint32_t)((((uint64_t)v.w << 32) | v.z) >> rs);
+  const uint32_t d4 = (uint32_t)((uint64_t)v.w >> rs);
+  const uint32_t m0 = ru_lowbytes(e < 4u ? e : 4u) & ~ru_lowbytes(o);
+  const uint32_t m1 = ru_lowbytes(e > 4u ? e - 4u : 0u);
+  const uint32_t m2 = ru_lowbytes(e > 8u ? e - 8u : 0u);
+  const uint32_t m3 = ru_lowbytes(e > 12u ? e - 12u : 0u);
+  const uint32_t m4 = ru_lowbytes(e > 16u ? e - 16u : 0u);
+  asm volatile(
+      "ds_mskor_b32 %0, %1, %2\n\t"
+      "ds_mskor_b32 %0, %3, %4 offset:4\n\t"
+      "ds_mskor_b32 %0, %5, %6 offset:8\n\t"
+      "ds_mskor_b32 %0, %7, %8 offset:12\n\t"
+      "ds_mskor_b32 %0, %9, %10 offset:16"
+      :
+      : "v"(addr), "v"(m0), "v"(d0 & m0), "v"(m1), "v"(d1 & m1), "v"(m2), "v"(d2 & m2), "v"(m3),
+        "v"(d3 & m3), "v"(m4), "v"(d4 & m4)
+      : "memory");
+}
+
 // one unit: its 16-byte source (LDS, final) -> its destination
+template <bool ALL5 = false>
 __device__ __forceinline__ void ru_copy(uint8_t* __restrict__ buf, uint32_t di, uint32_t n, uint32_t dist,
                                         bool per, const uint4* __restrict__ sel) {
   uint4 v = ru_rd16(buf, di - dist);
   if (per) v = ru_periodic(v, dist, sel);
-  ru_put(buf, di, n, v);
+  if (ALL5) ru_put5(buf, di, n, v);
+  else ru_put(buf, di, n, v);
 }
 
 #ifndef HBAM_RU_WAVES
 #define HBAM_RU_WAVES 8
+#endif
+#ifndef HBAM_RU_SROUND
+#define HBAM_RU_SROUND 0
 #endif
 __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const BlockRec* __restrict__ blk,
                                                                      const uint64_t* __restrict__ uoff, uint32_t nblk,
@@ -289,6 +321,25 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
       }
       const uint64_t need = (hi > lo && mine) ? ((hi - lo == 64u ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo) : 0ull;
       uint64_t done = ~__ballot(mine);
+#if HBAM_RU_SROUND
+      // the round's bookkeeping as wave-uniform masks: one compare + ballot gives the ready set,
+      // the copy runs under one exec mask with all five writes issued (no per-dword branches)
+      const uint64_t lbit = 1ull << lane;
+      for (;;) {
+        const uint64_t rb = __ballot((done & need) == need) & ~done;
+        if (rb == 0ull) {  // validated descriptors always make progress: corrupt
+          if (lane == 0) status[b] = INF_DATA;
+          return;
+        }
+        if (rb & lbit) ru_copy<true>(s_buf, lbase + q, n, dist, per, s_sel);
+        rs_lds_order();
+        done |= rb;
+#ifdef HBAM_PROF
+        ++n_bat;
+#endif
+        if (done == ~0ull) break;
+      }
+#else
       bool fin = !mine;
       for (;;) {
         const bool ready = !fin && (done & need) == need;
@@ -306,6 +357,7 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
           return;
         }
       }
+#endif
     } else if (nord) {
       // more than 64: a pending-byte bitmap over the stretch (+ spill); unit lane + 64 t
       for (uint32_t w = lane; w < RS_PW; w += 64) s_pend[w] = 0u;

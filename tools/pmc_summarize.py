@@ -27,7 +27,7 @@ import os
 import sys
 
 HBM_ACHIEVABLE = 6.3e12
-STAGE_OF = {"k_inflate_wave": "huffman_ms", "k_inflate_tokens": "huffman_ms", "k_resolve": "resolve_ms", "k_decode_pools": "pools_ms",
+STAGE_OF = {"k_inflate_wave": "huffman_ms", "k_inflate_tokens": "huffman_ms", "k_resolve": "resolve_ms", "k_resolve_units": "resolve_ms", "k_decode_pools": "pools_ms",
             "k_decode_fixed": "decode_ms", "k_scan_chunks": "scan_ms"}
 
 
@@ -74,6 +74,9 @@ def main():
     json.dump({"tree": tree, "comp_bytes": int(comp), "note": note, "kernels": res},
               open(os.path.join(outdir, "pmc_kernels.json"), "w"), indent=1)
     h = res.get("k_inflate_tokens")
+    hw = res.get("k_inflate_wave")
+    if hw and h and hw["hbm_bytes_per_launch"] < 0.01 * h["hbm_bytes_per_launch"]:
+        del res["k_inflate_wave"]  # only a small call (the header probe) took the wave pass
     if h and "k_inflate_wave" not in res:  # a call above HBAM_WAVE_MAX_BLOCKS: the lane pass alone
         one = {"kernel": "k_inflate_tokens", "tree": tree, "comp_bytes": int(comp),
                "fetch_bytes_per_launch": h["fetch_bytes"], "write_bytes_per_launch": h["write_bytes"],
