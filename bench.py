@@ -269,6 +269,8 @@ def main():
                          "shape; 12.5e9 = config #5's per-GPU share at 8 GPUs)")
     ap.add_argument("--sort-steps", type=int, default=2)
     ap.add_argument("--no-sort", action="store_true", help="N > 1: skip the Sort leg")
+    ap.add_argument("--sort-timeout", type=float, default=600.0,
+                    help="N > 1: seconds before the Sort leg's watchdog ends the ranks (the line is printed)")
     ap.add_argument("--config4", action="store_true",
                     help="BASELINE config #4 instead of the headline: ONE --c4-total file sharded over the N "
                          "GPUs (strong scaling), each rank's share resident, decoded in windows (tools/config4.py)")
@@ -405,20 +407,62 @@ def main():
             del whole
         except Exception as e:  # reported, never hidden
             parity = {"error": str(e)}
-    sort_leg = None
+    result = headline(args, world, elapsed, stages, huff_ms, ubytes, n_rec, own_len, file_len,
+                      ub_all, rec_all, parity) if rank == 0 else None
+    del cols
     if dist and not args.no_sort:
         # config #5's leg across the ranks (cli/plugins/Sort.java:131-170), after the headline's timed
         # region: decode + device sort + split points + exchange by key range (hbam_sort_exchange
         # over RCCL on nccl), with its own parity (tools/sort_leg.py)
-        import sort_leg as sl
-        del cols
-        sort_leg = sl.run(ctx, dist, rank, world, int(args.sort_size), args.seed + 101, threads, dev, cdev,
-                          N_REF, steps=args.sort_steps, log=log)
-    if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
+        res = guarded_sort_leg(ctx, dist, rank, world, args, threads, dev, cdev, result)
+        if rank == 0:
+            result["sort"] = res
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:  # the CPU baseline: rank 0 at N = 1 only
+            try:
+                result["cpu_baseline"] = cpu_baseline(buf, args.cpu_budget, threads)
+            except Exception as e:  # baseline is reported, never the target
+                result["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
+
+def guarded_sort_leg(ctx, dist, rank, world, args, threads, dev, cdev, result):
+    """The Sort leg under a watchdog.  Its exchange runs through libhbam's own RCCL communicator,
+    which has no timeout of its own: if a rank fails, the others would wait in a collective for
+    ever.  An exception is reported in the line (never hidden); a leg that has not finished after
+    --sort-timeout seconds ends every rank's process (rank 0 first prints the headline line with
+    the Sort leg's error), so the headline measurement is never lost to the leg."""
+    import threading
+    import sort_leg as sl
+    done = threading.Event()
+
+    def fire():
+        if done.is_set():
+            return
+        if rank == 0 and result is not None:
+            result["sort"] = {"error": "timeout after %.0f s" % args.sort_timeout}
+            print(json.dumps(result), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+    tm = threading.Timer(args.sort_timeout, fire)
+    tm.daemon = True
+    tm.start()
+    try:
+        return sl.run(ctx, dist, rank, world, int(args.sort_size), args.seed + 101, threads, dev, cdev,
+                      N_REF, steps=args.sort_steps, log=log)
+    except Exception as e:  # reported in the line, never hidden
+        log("sort leg rank %d failed: %s: %s" % (rank, type(e).__name__, e))
+        return {"error": "%s: %s" % (type(e).__name__, e)}
+    finally:
+        done.set()
+        tm.cancel()
+
+
+def headline(args, world, elapsed, stages, huff_ms, ubytes, n_rec, own_len, file_len, ub_all, rec_all, parity):
+    """rank 0: the bench line of the timed decode (value, stages, roofline, parity)"""
     per_step = elapsed / args.steps
     value = ub_all / per_step / 1e9
     avg = {k: float(np.mean([s[k] for s in stages])) for k in stages[0] if isinstance(stages[0][k], float)}
@@ -484,16 +528,7 @@ def main():
                                   "what": "C + 2U + columns/pools over the whole decode"}},
         "parity": parity,
     }
-    if sort_leg is not None:
-        result["sort"] = sort_leg
-    if not args.no_cpu_baseline:
-        try:
-            result["cpu_baseline"] = cpu_baseline(buf, args.cpu_budget, threads)
-        except Exception as e:  # baseline is reported, never the target
-            result["cpu_baseline"] = {"error": str(e)}
-    print(json.dumps(result), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    return result
 
 
 if __name__ == "__main__":

@@ -833,6 +833,16 @@ static __device__ __forceinline__ void st_part(uint8_t* d, uint32_t n, u32x4_a1 
   if (n & 2u) { *(u16_a1*)d = (uint16_t)lo; d += 2; lo >>= 16; }
   if (n & 1u) *d = (uint8_t)lo;
 }
+// the same through a global-address-space pointer (global_store_*, never flat_store_*: flat
+// operations retire out of order, which hand-counted vmcnt waits cannot allow)
+#define HBAM_G __attribute__((address_space(1)))
+static __device__ __forceinline__ void st_part_g(HBAM_G uint8_t* d, uint32_t n, u32x4_a1 v) {  // n < 16
+  uint64_t lo = (uint64_t)v[0] | (uint64_t)v[1] << 32, hi = (uint64_t)v[2] | (uint64_t)v[3] << 32;
+  if (n & 8u) { *(HBAM_G u64_a1*)d = lo; d += 8; lo = hi; }
+  if (n & 4u) { *(HBAM_G u32_a1*)d = (uint32_t)lo; d += 4; lo >>= 32; }
+  if (n & 2u) { *(HBAM_G u16_a1*)d = (uint16_t)lo; d += 2; lo >>= 16; }
+  if (n & 1u) *d = (uint8_t)lo;
+}
 // 4 SEQ characters of the packed bytes b0 (high nibble first) and b1
 static __device__ __forceinline__ uint32_t seq4(uint32_t b0, uint32_t b1) {
   // "=ACMGRSVTWYHKDBN" as two 8-byte halves for v_perm (selector byte = nibble & 7)
@@ -860,6 +870,10 @@ static __device__ __forceinline__ u32x4_a1 seq16(const uint8_t* __restrict__ s) 
 // with units, and a unit finds its record's rank as a popcount: the records whose first unit lies
 // in the 64-unit window are one bit each of a mask (distinct positions), the earlier ones are
 // counted by one ballot.  One ds_read_b128 per unit.
+#ifndef HBAM_POOLS_U
+#define HBAM_POOLS_U 1
+#endif
+static_assert(HBAM_POOLS_U >= 1 && HBAM_POOLS_U <= 4, "pools: 1-4 windows per step (the waits below)");
 static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
   return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l) << 32;
@@ -912,6 +926,69 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
       asm volatile("" ::: "memory");  // (one wave: its LDS operations run in issue order)
       uint8_t* const dbase = base + db;
       const uint8_t* const sbase = u + sb;
+#if HBAM_POOLS_U > 1
+      // HBAM_POOLS_U windows per step, every load issued before the first store.  With one
+      // window per step the compiler puts s_waitcnt vmcnt(0) ahead of each load (the address is
+      // built by VALU writes into registers that held the last store's data, which the store
+      // reads late), so every step paid a load round trip plus a store acknowledgement.  The
+      // loads here are asm with early-clobber outputs (only the load writes them), one per window
+      // that has units (V of them, a prefix; every lane loads, lanes without a unit from a valid
+      // dummy address), so the waits can be counted by hand: younger than load w are the V-1-w
+      // later loads and at least one store per earlier window (lane 0 of a window with units
+      // always stores), so vmcnt(V-1) is enough for every w < V, and no load is left in flight
+      // once the step's stores are issued (a late load would write registers the compiler has
+      // reused).
+      for (uint32_t q0 = 0; q0 < total; q0 += 64 * HBAM_POOLS_U) {
+        u32x4_t raw[HBAM_POOLS_U];
+        uint8_t* dp[HBAM_POOLS_U];
+        uint32_t nn[HBAM_POOLS_U];
+        const uint32_t nv = (total - q0 + 63u) / 64u, V = nv < HBAM_POOLS_U ? nv : HBAM_POOLS_U;
+#pragma unroll
+        for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
+          nn[w] = 0;
+          dp[w] = dbase;
+          if (w >= V) continue;  // wave-uniform
+          const uint32_t qw = q0 + 64u * w;
+          const uint8_t* sp = sbase;
+          const uint32_t q = qw + lane;
+          const uint32_t pos = excl - qw;
+          const bool inwin = has && excl >= qw && pos < 64u;
+          const uint32_t blo = (inwin && pos < 32u) ? 1u << pos : 0u;
+          const uint32_t bhi = (inwin && pos >= 32u) ? 1u << (pos - 32u) : 0u;
+          const uint64_t M = (uint64_t)wave_last(wave_scan_dpp(bhi)) << 32 | wave_last(wave_scan_dpp(blo));
+          const uint32_t c0 = (uint32_t)__popcll(__ballot(has && excl < qw));
+          if (q < total) {
+            const uint4 rr = recs[c0 + (uint32_t)__popcll(M & le) - 1u];
+            const uint32_t k = q - rr.w;
+            nn[w] = rr.z - 16u * k;
+            dp[w] = dbase + rr.y + 16u * k;
+            sp = sbase + rr.x + (f == 2 ? 8u : 16u) * k;
+          }
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(raw[w]) : "v"(sp) : "memory");
+        }
+#pragma unroll
+        for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
+          if (w >= V) break;  // wave-uniform
+          // the operand ties the data to the wait
+          if (V == 1) asm volatile("s_waitcnt vmcnt(0)" : "+v"(raw[w]) : : "memory");
+          else if (V == 2) asm volatile("s_waitcnt vmcnt(1)" : "+v"(raw[w]) : : "memory");
+          else if (V == 3) asm volatile("s_waitcnt vmcnt(2)" : "+v"(raw[w]) : : "memory");
+          else asm volatile("s_waitcnt vmcnt(3)" : "+v"(raw[w]) : : "memory");
+          u32x4_a1 v;
+          if (f == 2) {
+            const uint64_t qq = (uint64_t)raw[w][0] | (uint64_t)raw[w][1] << 32;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              v[j] = seq4((uint32_t)(qq >> (16 * j)) & 0xffu, (uint32_t)(qq >> (16 * j + 8)) & 0xffu);
+          } else {
+            v = u32x4_a1{raw[w][0], raw[w][1], raw[w][2], raw[w][3]};
+          }
+          HBAM_G uint8_t* const gd = (HBAM_G uint8_t*)dp[w];
+          if (nn[w] >= 16u) *(HBAM_G u32x4_a1*)gd = v;
+          else if (nn[w] != 0u) st_part_g(gd, nn[w], v);
+        }
+      }
+#else
       for (uint32_t q0 = 0; q0 < total; q0 += 64) {
         const uint32_t q = q0 + lane;
         // the window's record starts, one bit each, and the records that start before it
@@ -930,6 +1007,7 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
           else st_part(dp, n, v);
         }
       }
+#endif
     }
   }
 }

@@ -42,7 +42,11 @@ __device__ __forceinline__ uint4 ru_rd16(const uint8_t* buf, uint32_t x) {
   // hide the 4-byte alignment from the compiler, which would otherwise split the read into a
   // misaligned ds_read_b64 + ds_read2_b32: one ds_read_b128 at dword alignment runs at full rate
   asm("" : "+v"(a));
-  const uint4 q = *(const uint4*)(buf + a);
+  // an ext_vector load carries align 16 in the IR (uint4 is a struct of four u32: align 4, which
+  // the backend split into ds_read_b64 + ds_read2_b32 pairs; A/B at 5 GB, with the scalar-mask
+  // rounds below: 15.52 -> 15.34 ms, profiles/r05/ab/resolve_sround_b128_5g.txt)
+  const u32x4_t qv = *(const u32x4_t*)(buf + a);
+  const uint4 q = make_uint4(qv[0], qv[1], qv[2], qv[3]);
   const uint32_t q4 = *(const uint32_t*)(buf + a + 16u);
   return make_uint4(__builtin_amdgcn_alignbit(q.y, q.x, sh), __builtin_amdgcn_alignbit(q.z, q.y, sh),
                     __builtin_amdgcn_alignbit(q.w, q.z, sh), __builtin_amdgcn_alignbit(q4, q.w, sh));
@@ -126,9 +130,7 @@ __device__ __forceinline__ void ru_copy(uint8_t* __restrict__ buf, uint32_t di, 
 #ifndef HBAM_RU_WAVES
 #define HBAM_RU_WAVES 8
 #endif
-#ifndef HBAM_RU_SROUND
-#define HBAM_RU_SROUND 0
-#endif
+
 __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const BlockRec* __restrict__ blk,
                                                                      const uint64_t* __restrict__ uoff, uint32_t nblk,
                                                                      uint8_t* __restrict__ ubuf,
@@ -321,9 +323,10 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
       }
       const uint64_t need = (hi > lo && mine) ? ((hi - lo == 64u ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo) : 0ull;
       uint64_t done = ~__ballot(mine);
-#if HBAM_RU_SROUND
       // the round's bookkeeping as wave-uniform masks: one compare + ballot gives the ready set,
-      // the copy runs under one exec mask with all five writes issued (no per-dword branches)
+      // the copy runs under one exec mask with all five writes issued (no per-dword branches);
+      // against per-lane ready/fin flags: ordered phase 600k -> 555k cycles per block, resolve
+      // 15.63 -> 15.44 ms at 5 GB (profiles/r05/ab/resolve_sround_5g.txt)
       const uint64_t lbit = 1ull << lane;
       for (;;) {
         const uint64_t rb = __ballot((done & need) == need) & ~done;
@@ -339,25 +342,6 @@ __global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const Block
 #endif
         if (done == ~0ull) break;
       }
-#else
-      bool fin = !mine;
-      for (;;) {
-        const bool ready = !fin && (done & need) == need;
-        if (ready) ru_copy(s_buf, lbase + q, n, dist, per, s_sel);
-        rs_lds_order();
-        fin = fin || ready;
-        const uint64_t rb = __ballot(ready);
-        done |= rb;
-#ifdef HBAM_PROF
-        ++n_bat;
-#endif
-        if (!__any(!fin)) break;
-        if (rb == 0ull) {  // validated descriptors always make progress: corrupt
-          if (lane == 0) status[b] = INF_DATA;
-          return;
-        }
-      }
-#endif
     } else if (nord) {
       // more than 64: a pending-byte bitmap over the stretch (+ spill); unit lane + 64 t
       for (uint32_t w = lane; w < RS_PW; w += 64) s_pend[w] = 0u;

@@ -155,15 +155,20 @@ def test_inflate_every_output_misalignment(gpu_ctx, fname):
             assert u[int(off[j]):int(off[j + 1])].tobytes() == want[b[0]], (lead, j)
 
 
-def test_inflate_independent_of_launch_position(gpu_ctx, oracle_mod, genbam):
+@pytest.mark.parametrize("mode", ["lane", "wave"])
+def test_inflate_independent_of_launch_position(oracle_mod, genbam, monkeypatch, mode):
     """The r02 profiling-build failure depended on a block's position in the
     launch, not on its bytes: only waves that started in a slot an earlier wave of the launch
     had vacated decoded wrongly.  Here the same blocks (zlib levels 1/5/9, uniform and binned
     qualities, stored and fixed-Huffman blocks) are repeated until the launch holds ~2.7
-    waves per slot of the whole chip (2 waves/SIMD x 4 SIMDs x 256 CUs), so most copies run in a
-    reused slot; every copy must inflate CRC-clean on the device (status 0)."""
+    waves per slot of the whole chip (2 waves/SIMD x 4 SIMDs x 256 CUs) for the lane pass
+    (k_inflate_tokens), and 350,000 one-block waves for the wave pass (k_inflate_wave, forced by
+    HBAM_WAVE_MAX_BLOCKS), so most copies run in a reused slot; every copy must inflate
+    CRC-clean on the device (status 0)."""
     import ctypes as C
     from hadoop_bam import _lib
+    monkeypatch.setenv("HBAM_WAVE_MAX_BLOCKS", "1000000000" if mode == "wave" else "0")
+    gpu_ctx = _lib.Context(0)
     parts = [np.asarray(genbam.generate(records=4000, seed=31, level=1)),
              np.asarray(genbam.generate(records=4000, seed=32, level=9, uniform_qual=1)),
              np.asarray(genbam.generate(records=1500, seed=33, level=0)),
@@ -185,11 +190,14 @@ def test_inflate_independent_of_launch_position(gpu_ctx, oracle_mod, genbam):
         arr[i].coff, arr[i].clen, arr[i].isize, arr[i].crc = coffs[j], int(clens[j]), int(isz[j]), int(crcs[j])
     off = np.zeros(n + 1, np.uint64)
     st = np.full(n, 99, np.int32)
-    rc = gpu_ctx.L.hbam_inflate(gpu_ctx.h, C.c_void_p(data.ctypes.data), 0, len(data), arr, n, 1,
-                                None, 0, off.ctypes.data, st.ctypes.data)
-    assert rc == 0, gpu_ctx.last_error()
-    bad = np.nonzero(st != 0)[0]
-    assert len(bad) == 0, (len(bad), n, bad[:8], st[bad[:8]])
+    try:
+        rc = gpu_ctx.L.hbam_inflate(gpu_ctx.h, C.c_void_p(data.ctypes.data), 0, len(data), arr, n, 1,
+                                    None, 0, off.ctypes.data, st.ctypes.data)
+        assert rc == 0, gpu_ctx.last_error()
+        bad = np.nonzero(st != 0)[0]
+        assert len(bad) == 0, (mode, len(bad), n, bad[:8], st[bad[:8]])
+    finally:
+        gpu_ctx.close()
 
 
 @pytest.mark.parametrize("kw", [dict(level=0), dict(level=1), dict(level=9),

@@ -22,6 +22,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--seed", type=int, default=2)
 ap.add_argument("--libs", nargs="+", default=["libhbam.so"])
 ap.add_argument("--digest", type=int, default=1)
+ap.add_argument("--addr", type=int, default=1, help="print the output buffers' device addresses")
 a = ap.parse_args()
 g = genbam.generate(target_bytes=int(a.size), seed=a.seed, threads=16)
 data = np.asarray(g)
@@ -40,6 +41,11 @@ for lib in a.libs:
     for r in range(a.reps):
         rc, cols = ctx.decode_split_device(d[:len(data)], v0, v1, h["n_ref"])
         t = ctx.timing()
+        if r == 0 and a.addr:  # where the pools kernel's buffers landed (placement A/B)
+            ad = {k: C.cast(getattr(cols, k), C.c_void_p).value or 0
+                  for k in ("ubuf", "rec_off", "names", "cigars", "seq", "qual", "aux", "name_off", "seq_off")}
+            print("%-18s addr %s" % (lib, " ".join("%s=%x(%%2M=%x)" % (k, v, v % (2 << 20)) for k, v in ad.items())),
+                  flush=True)
         print("%-18s rep %d rc %d n %d total %.3f ms  scan %.3f huffman %.3f resolve %.3f walk %.3f "
               "decode %.3f pools %.3f" % (lib, r, rc, cols.n_records, t["total_ms"], t["scan_ms"],
                                           t["huffman_ms"], t["resolve_ms"], t["walk_ms"], t["decode_ms"],
