@@ -826,15 +826,8 @@ __global__ void k_decode_fixed(const uint8_t* __restrict__ u, uint64_t nrec,
 // 10 GB shard, every store instruction touching 64 lines.)
 typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 typedef uint64_t u64_a1 __attribute__((aligned(1)));
-static __device__ __forceinline__ void st_part(uint8_t* d, uint32_t n, u32x4_a1 v) {  // n < 16
-  uint64_t lo = (uint64_t)v[0] | (uint64_t)v[1] << 32, hi = (uint64_t)v[2] | (uint64_t)v[3] << 32;
-  if (n & 8u) { *(u64_a1*)d = lo; d += 8; lo = hi; }
-  if (n & 4u) { *(u32_a1*)d = (uint32_t)lo; d += 4; lo >>= 32; }
-  if (n & 2u) { *(u16_a1*)d = (uint16_t)lo; d += 2; lo >>= 16; }
-  if (n & 1u) *d = (uint8_t)lo;
-}
-// the same through a global-address-space pointer (global_store_*, never flat_store_*: flat
-// operations retire out of order, which hand-counted vmcnt waits cannot allow)
+// the first n < 16 bytes of v in 8/4/2/1-byte pieces, through a global-address-space pointer
+// (global_store_*: a generic pointer made them flat_store_*)
 #define HBAM_G __attribute__((address_space(1)))
 static __device__ __forceinline__ void st_part_g(HBAM_G uint8_t* d, uint32_t n, u32x4_a1 v) {  // n < 16
   uint64_t lo = (uint64_t)v[0] | (uint64_t)v[1] << 32, hi = (uint64_t)v[2] | (uint64_t)v[3] << 32;
@@ -854,14 +847,6 @@ static __device__ __forceinline__ uint32_t seq4(uint32_t b0, uint32_t b1) {
                      ((n3 >> 3) * 0xffu) << 24;
   return (lo & ~m) | (hi & m);
 }
-// 16 SEQ characters (or the first n < 16 of them) of the packed bytes at s (8 bytes read)
-static __device__ __forceinline__ u32x4_a1 seq16(const uint8_t* __restrict__ s) {
-  const uint64_t q = *(const u64_a1*)s;
-  u32x4_a1 o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = seq4((uint32_t)(q >> (16 * j)) & 0xffu, (uint32_t)(q >> (16 * j + 8)) & 0xffu);
-  return o;
-}
 // The unit -> record mapping without the LDS pipe's shuffles (round 5; the round-4 kernel spent
 // ~11 ds_bpermute per 64 units on a 6-step binary search over the lanes' first units plus the
 // record's fields, and 7 per field scan: 9.17 -> 8.87 ms at 5 GB, same pools,
@@ -871,9 +856,9 @@ static __device__ __forceinline__ u32x4_a1 seq16(const uint8_t* __restrict__ s) 
 // in the 64-unit window are one bit each of a mask (distinct positions), the earlier ones are
 // counted by one ballot.  One ds_read_b128 per unit.
 #ifndef HBAM_POOLS_U
-#define HBAM_POOLS_U 1
-#endif
-static_assert(HBAM_POOLS_U >= 1 && HBAM_POOLS_U <= 4, "pools: 1-4 windows per step (the waits below)");
+#define HBAM_POOLS_U 4  // windows per step; A/B at 5 GB, pools ms: 1 9.34, 2 8.57, 3 8.88, 4 8.51
+#endif                  // (profiles/r05/ab/pools_windows_per_step_5g.txt; same pools in every build)
+static_assert(HBAM_POOLS_U >= 2 && HBAM_POOLS_U <= 4, "pools: 2-4 windows per step (the load asm below)");
 static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
   return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l) << 32;
@@ -926,30 +911,26 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
       asm volatile("" ::: "memory");  // (one wave: its LDS operations run in issue order)
       uint8_t* const dbase = base + db;
       const uint8_t* const sbase = u + sb;
-#if HBAM_POOLS_U > 1
-      // HBAM_POOLS_U windows per step, every load issued before the first store.  With one
-      // window per step the compiler puts s_waitcnt vmcnt(0) ahead of each load (the address is
-      // built by VALU writes into registers that held the last store's data, which the store
-      // reads late), so every step paid a load round trip plus a store acknowledgement.  The
-      // loads here are asm with early-clobber outputs (only the load writes them), one per window
-      // that has units (V of them, a prefix; every lane loads, lanes without a unit from a valid
-      // dummy address), so the waits can be counted by hand: younger than load w are the V-1-w
-      // later loads and at least one store per earlier window (lane 0 of a window with units
-      // always stores), so vmcnt(V-1) is enough for every w < V, and no load is left in flight
-      // once the step's stores are issued (a late load would write registers the compiler has
-      // reused).
+      // HBAM_POOLS_U windows per step, their loads issued back to back before any store.  With
+      // one window per step the compiler puts s_waitcnt vmcnt(0) ahead of each load (the address
+      // is built by VALU writes into registers that held the last store's data, which the store
+      // reads late), so every step paid a load round trip plus a store acknowledgement.  The U
+      // loads and their wait are ONE asm statement (lanes and windows without a unit read a valid
+      // dummy address): nothing the compiler schedules can touch the destinations between a load
+      // and its data (a wait in a separate statement let it copy the registers before the data
+      // had landed), and no load is left in flight after the statement.
       for (uint32_t q0 = 0; q0 < total; q0 += 64 * HBAM_POOLS_U) {
         u32x4_t raw[HBAM_POOLS_U];
+        const uint8_t* sp[HBAM_POOLS_U];
         uint8_t* dp[HBAM_POOLS_U];
         uint32_t nn[HBAM_POOLS_U];
-        const uint32_t nv = (total - q0 + 63u) / 64u, V = nv < HBAM_POOLS_U ? nv : HBAM_POOLS_U;
 #pragma unroll
         for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
           nn[w] = 0;
           dp[w] = dbase;
-          if (w >= V) continue;  // wave-uniform
+          sp[w] = sbase;
           const uint32_t qw = q0 + 64u * w;
-          const uint8_t* sp = sbase;
+          if (qw >= total) continue;  // wave-uniform
           const uint32_t q = qw + lane;
           const uint32_t pos = excl - qw;
           const bool inwin = has && excl >= qw && pos < 64u;
@@ -962,18 +943,25 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
             const uint32_t k = q - rr.w;
             nn[w] = rr.z - 16u * k;
             dp[w] = dbase + rr.y + 16u * k;
-            sp = sbase + rr.x + (f == 2 ? 8u : 16u) * k;
+            sp[w] = sbase + rr.x + (f == 2 ? 8u : 16u) * k;
           }
-          asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(raw[w]) : "v"(sp) : "memory");
         }
+#if HBAM_POOLS_U == 2
+        asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off\n\ts_waitcnt vmcnt(0)"
+                     : "=&v"(raw[0]), "=&v"(raw[1]) : "v"(sp[0]), "v"(sp[1]) : "memory");
+#elif HBAM_POOLS_U == 3
+        asm volatile("global_load_dwordx4 %0, %3, off\n\tglobal_load_dwordx4 %1, %4, off\n\t"
+                     "global_load_dwordx4 %2, %5, off\n\ts_waitcnt vmcnt(0)"
+                     : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]) : "v"(sp[0]), "v"(sp[1]), "v"(sp[2]) : "memory");
+#else
+        asm volatile("global_load_dwordx4 %0, %4, off\n\tglobal_load_dwordx4 %1, %5, off\n\t"
+                     "global_load_dwordx4 %2, %6, off\n\tglobal_load_dwordx4 %3, %7, off\n\ts_waitcnt vmcnt(0)"
+                     : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]), "=&v"(raw[3])
+                     : "v"(sp[0]), "v"(sp[1]), "v"(sp[2]), "v"(sp[3]) : "memory");
+#endif
 #pragma unroll
         for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
-          if (w >= V) break;  // wave-uniform
-          // the operand ties the data to the wait
-          if (V == 1) asm volatile("s_waitcnt vmcnt(0)" : "+v"(raw[w]) : : "memory");
-          else if (V == 2) asm volatile("s_waitcnt vmcnt(1)" : "+v"(raw[w]) : : "memory");
-          else if (V == 3) asm volatile("s_waitcnt vmcnt(2)" : "+v"(raw[w]) : : "memory");
-          else asm volatile("s_waitcnt vmcnt(3)" : "+v"(raw[w]) : : "memory");
+          if (q0 + 64u * w >= total) break;  // wave-uniform
           u32x4_a1 v;
           if (f == 2) {
             const uint64_t qq = (uint64_t)raw[w][0] | (uint64_t)raw[w][1] << 32;
@@ -988,26 +976,6 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
           else if (nn[w] != 0u) st_part_g(gd, nn[w], v);
         }
       }
-#else
-      for (uint32_t q0 = 0; q0 < total; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        // the window's record starts, one bit each, and the records that start before it
-        const uint32_t pos = excl - q0;
-        const bool inwin = has && excl >= q0 && pos < 64u;
-        const uint32_t blo = (inwin && pos < 32u) ? 1u << pos : 0u;
-        const uint32_t bhi = (inwin && pos >= 32u) ? 1u << (pos - 32u) : 0u;
-        const uint64_t M = (uint64_t)wave_last(wave_scan_dpp(bhi)) << 32 | wave_last(wave_scan_dpp(blo));
-        const uint32_t c0 = (uint32_t)__popcll(__ballot(has && excl < q0));
-        if (q < total) {
-          const uint4 rr = recs[c0 + (uint32_t)__popcll(M & le) - 1u];
-          const uint32_t k = q - rr.w, n = rr.z - 16u * k;
-          uint8_t* dp = dbase + rr.y + 16u * k;
-          const u32x4_a1 v = f == 2 ? seq16(sbase + rr.x + 8u * k) : *(const u32x4_a1*)(sbase + rr.x + 16u * k);
-          if (n >= 16u) *(u32x4_a1*)dp = v;
-          else st_part(dp, n, v);
-        }
-      }
-#endif
     }
   }
 }

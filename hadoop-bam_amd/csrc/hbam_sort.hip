@@ -150,6 +150,9 @@ typedef uint32_t g_u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 typedef uint64_t g_u64_a1 __attribute__((aligned(1)));
 typedef uint32_t g_u32_a1 __attribute__((aligned(1)));
 typedef uint16_t g_u16_a1 __attribute__((aligned(1)));
+#ifndef HBAM_GATHER2
+#define HBAM_GATHER2 0
+#endif
 __global__ __launch_bounds__(256) void k_gather_records_tile(const uint8_t* __restrict__ ubuf,
                                                              const uint64_t* __restrict__ rec_off,
                                                              const uint32_t* __restrict__ perm, uint64_t n,
@@ -158,6 +161,83 @@ __global__ __launch_bounds__(256) void k_gather_records_tile(const uint8_t* __re
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t ntiles = (n + 63) / 64;
   const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
+#if HBAM_GATHER2
+  // The pools kernel's unit mapping (hbam_kernels.hip, k_decode_pools): DPP scans, each record's
+  // (source, destination, bytes, first unit) once in LDS at its rank, a unit's record by popcount;
+  // two 64-unit windows per step with both loads (random sources: the permuted records) and their
+  // wait in one asm statement.
+  __shared__ uint4 s_rec[4][64];
+  __shared__ uint32_t s_first[4][64];
+  uint4* const recs = s_rec[threadIdx.x >> 6];
+  uint32_t* const firsts = s_first[threadIdx.x >> 6];
+  const uint64_t le = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); t < ntiles; t += wstride) {
+    const uint64_t i = t * 64 + lane;
+    uint64_t src = 0, dst = 0;
+    uint32_t len = 0;
+    if (i < n) {
+      src = rec_off[perm ? perm[i] : i];
+      dst = out_off[i];
+      len = (uint32_t)(out_off[i + 1] - dst);
+    }
+    const uint32_t units = (len + 15u) >> 4;
+    const uint32_t incl = wave_scan_dpp(units), excl = incl - units, total = wave_last(incl);
+    if (total == 0u) continue;
+    const bool has = units != 0u;
+    const uint64_t mh = __ballot(has);
+    const uint32_t first = (uint32_t)__builtin_ctzll(mh);
+    const uint64_t db = readlane64(dst, first);  // (zero-extends the low half: dst passes 2^31)
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");  // the previous tile's reads of the table precede these writes
+    if (has) {
+      const uint32_t rk = lane_rank(mh);
+      recs[rk] = make_uint4((uint32_t)src, (uint32_t)(src >> 32), (uint32_t)(dst - db), len);
+      firsts[rk] = excl;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    uint8_t* const obase = out + db;
+    for (uint32_t q0 = 0; q0 < total; q0 += 128) {
+      u32x4_t raw[2];
+      const uint8_t* sp[2];
+      uint8_t* dp[2];
+      uint32_t nn[2];
+#pragma unroll
+      for (uint32_t w = 0; w < 2; ++w) {
+        nn[w] = 0;
+        dp[w] = obase;
+        sp[w] = ubuf;  // valid dummy address
+        const uint32_t qw = q0 + 64u * w;
+        if (qw >= total) continue;  // wave-uniform
+        const uint32_t q = qw + lane;
+        const uint32_t pos = excl - qw;
+        const bool inwin = has && excl >= qw && pos < 64u;
+        const uint32_t blo = (inwin && pos < 32u) ? 1u << pos : 0u;
+        const uint32_t bhi = (inwin && pos >= 32u) ? 1u << (pos - 32u) : 0u;
+        const uint64_t M = (uint64_t)wave_last(wave_scan_dpp(bhi)) << 32 | wave_last(wave_scan_dpp(blo));
+        const uint32_t c0 = (uint32_t)__popcll(__ballot(has && excl < qw));
+        if (q < total) {
+          const uint32_t rk = c0 + (uint32_t)__popcll(M & le) - 1u;
+          const uint4 rr = recs[rk];
+          const uint32_t k = q - firsts[rk];
+          nn[w] = rr.w - 16u * k;
+          dp[w] = obase + rr.z + 16u * k;
+          sp[w] = ubuf + ((uint64_t)rr.x | (uint64_t)rr.y << 32) + 16u * k;
+        }
+      }
+      asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off\n\ts_waitcnt vmcnt(0)"
+                   : "=&v"(raw[0]), "=&v"(raw[1]) : "v"(sp[0]), "v"(sp[1]) : "memory");
+#pragma unroll
+      for (uint32_t w = 0; w < 2; ++w) {
+        if (q0 + 64u * w >= total) break;  // wave-uniform
+        const u32x4_a1 v = u32x4_a1{raw[w][0], raw[w][1], raw[w][2], raw[w][3]};
+        HBAM_G uint8_t* const gd = (HBAM_G uint8_t*)dp[w];
+        if (nn[w] >= 16u) *(HBAM_G u32x4_a1*)gd = v;
+        else if (nn[w] != 0u) st_part_g(gd, nn[w], v);
+      }
+    }
+  }
+#else
   for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); t < ntiles; t += wstride) {
     const uint64_t i = t * 64 + lane;
     uint64_t src = 0, dst = 0;
@@ -202,6 +282,7 @@ __global__ __launch_bounds__(256) void k_gather_records_tile(const uint8_t* __re
       }
     }
   }
+#endif
 }
 
 // TotalOrderPartitioner bounds: for split point j, the first index whose (signed) key is

@@ -209,8 +209,9 @@ __device__ __forceinline__ void huffp_make(const Huff& h, HuffP& p) {
   "v_pk_min_u16 %[g], %[g], %[one]\n\t"              \
   "v_dot2_u32_u16 %[sl], %[g], %[one], %[sl]\n\t"    \
   "v_dot2_u32_u16 %[so], %[g], " DOF ", %[so]\n\t"
-// Two pairs at a time with two compare registers (HBAM_TOK_ILV): the sub -> min -> dot2 chain of
-// one pair has the other pair's instructions between its links instead of stalling on them.
+// Two pairs at a time with two compare registers: the sub -> min -> dot2 chain of one pair has the
+// other pair's instructions between its links instead of stalling on them (A/B at 5 GB: Huffman
+// 34.1 -> 33.8 ms, same output; profiles/r05/ab/pools_windows_tok_ilv_5g.txt).
 #define HBAM_PK2_PAIR(LA, DA, TA, LB, DB, TB)          \
   "v_pk_sub_u16 %[g], %[vv], " LA " clamp\n\t"        \
   "v_pk_sub_u16 %[h], %[vv], " LB " clamp\n\t"        \
@@ -231,16 +232,12 @@ __device__ __forceinline__ void huffp_make(const Huff& h, HuffP& p) {
   "v_dot2_u32_u16 %[so], %[g], " DA ", %[so]\n\t"     \
   "v_dot2_u32_u16 %[sl], %[h], %[one], %[sl]\n\t"     \
   "v_dot2_u32_u16 %[so], %[h], " DB ", %[so]\n\t"
-#ifndef HBAM_TOK_ILV
-#define HBAM_TOK_ILV 0
-#endif
 template <bool HI>
 __device__ __forceinline__ bool huffp_lookup(const HuffP& h, uint32_t v, uint32_t& L, uint32_t& idx,
                                              uint32_t& hi) {
   const uint32_t vv = (v + 1u) * 0x10001u;  // v + 1 <= 32768 in both halves
   const uint32_t one = 0x10001u;
   uint32_t sl = 0, so = 0, st = 0, g;
-#if HBAM_TOK_ILV
   uint32_t g2;
   if (HI) {
     asm(HBAM_PK2_PAIR("%[l0]", "%[d0]", "%[t0]", "%[l1]", "%[d1]", "%[t1]")
@@ -265,33 +262,6 @@ __device__ __forceinline__ bool huffp_lookup(const HuffP& h, uint32_t v, uint32_
           [d0] "v"(h.dof[0]), [d1] "v"(h.dof[1]), [d2] "v"(h.dof[2]), [d3] "v"(h.dof[3]),
           [d4] "v"(h.dof[4]), [d5] "v"(h.dof[5]), [d6] "v"(h.dof[6]));
   }
-#else
-  if (HI) {
-    asm(HBAM_PK_PAIR("%[l0]", "%[d0]", "%[t0]") HBAM_PK_PAIR("%[l1]", "%[d1]", "%[t1]")
-        HBAM_PK_PAIR("%[l2]", "%[d2]", "%[t2]") HBAM_PK_PAIR("%[l3]", "%[d3]", "%[t3]")
-        : [sl] "+v"(sl), [so] "+v"(so), [st] "+v"(st), [g] "=&v"(g)
-        : [vv] "v"(vv), [one] "v"(one), [l0] "v"(h.lim[0]), [l1] "v"(h.lim[1]), [l2] "v"(h.lim[2]),
-          [l3] "v"(h.lim[3]), [d0] "v"(h.dof[0]), [d1] "v"(h.dof[1]), [d2] "v"(h.dof[2]),
-          [d3] "v"(h.dof[3]), [t0] "v"(h.dhl[0]), [t1] "v"(h.dhl[1]), [t2] "v"(h.dhl[2]),
-          [t3] "v"(h.dhl[3]));
-    asm(HBAM_PK_PAIR("%[l4]", "%[d4]", "%[t4]") HBAM_PK_PAIR("%[l5]", "%[d5]", "%[t5]")
-        HBAM_PK_PAIR("%[l6]", "%[d6]", "%[t6]")
-        : [sl] "+v"(sl), [so] "+v"(so), [st] "+v"(st), [g] "=&v"(g)
-        : [vv] "v"(vv), [one] "v"(one), [l4] "v"(h.lim[4]), [l5] "v"(h.lim[5]), [l6] "v"(h.lim[6]),
-          [d4] "v"(h.dof[4]), [d5] "v"(h.dof[5]), [d6] "v"(h.dof[6]), [t4] "v"(h.dhl[4]),
-          [t5] "v"(h.dhl[5]), [t6] "v"(h.dhl[6]));
-  } else {
-    asm(HBAM_PK_PAIR_NT("%[l0]", "%[d0]") HBAM_PK_PAIR_NT("%[l1]", "%[d1]")
-        HBAM_PK_PAIR_NT("%[l2]", "%[d2]") HBAM_PK_PAIR_NT("%[l3]", "%[d3]")
-        HBAM_PK_PAIR_NT("%[l4]", "%[d4]") HBAM_PK_PAIR_NT("%[l5]", "%[d5]")
-        HBAM_PK_PAIR_NT("%[l6]", "%[d6]")
-        : [sl] "+v"(sl), [so] "+v"(so), [g] "=&v"(g)
-        : [vv] "v"(vv), [one] "v"(one), [l0] "v"(h.lim[0]), [l1] "v"(h.lim[1]), [l2] "v"(h.lim[2]),
-          [l3] "v"(h.lim[3]), [l4] "v"(h.lim[4]), [l5] "v"(h.lim[5]), [l6] "v"(h.lim[6]),
-          [d0] "v"(h.dof[0]), [d1] "v"(h.dof[1]), [d2] "v"(h.dof[2]), [d3] "v"(h.dof[3]),
-          [d4] "v"(h.dof[4]), [d5] "v"(h.dof[5]), [d6] "v"(h.dof[6]));
-  }
-#endif
   const uint32_t l = 1u + sl;
   L = l;
   idx = (h.o0 + so + (v >> (15u - l))) & 0xffffu;
