@@ -141,18 +141,11 @@ __global__ __launch_bounds__(RS_WG) void k_perm_lens(const int32_t* __restrict__
 // consecutive output records (k_decode_pools' unit
 // scheme): each lane reads its record's source offset and length once, every record is cut into
 // 16-byte units numbered by a wave scan, and consecutive lanes take consecutive units (a unit's
-// record found by a 6-step shuffle search), so a wave instruction moves ~1 KiB of the output
+// record found by popcount, below), so a wave instruction moves ~1 KiB of the output
 // stream and the three dependent index loads are paid once per 64 records instead of once per
 // record.  A record's last unit may be shorter: written in 8/4/2/1-byte pieces, so a neighbour's
 // bytes are never written.  Source over-reads (up to 15 bytes past a record) stay inside ubuf +
 // its slack.
-typedef uint32_t g_u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
-typedef uint64_t g_u64_a1 __attribute__((aligned(1)));
-typedef uint32_t g_u32_a1 __attribute__((aligned(1)));
-typedef uint16_t g_u16_a1 __attribute__((aligned(1)));
-#ifndef HBAM_GATHER2
-#define HBAM_GATHER2 0
-#endif
 __global__ __launch_bounds__(256) void k_gather_records_tile(const uint8_t* __restrict__ ubuf,
                                                              const uint64_t* __restrict__ rec_off,
                                                              const uint32_t* __restrict__ perm, uint64_t n,
@@ -161,11 +154,11 @@ __global__ __launch_bounds__(256) void k_gather_records_tile(const uint8_t* __re
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t ntiles = (n + 63) / 64;
   const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
-#if HBAM_GATHER2
   // The pools kernel's unit mapping (hbam_kernels.hip, k_decode_pools): DPP scans, each record's
   // (source, destination, bytes, first unit) once in LDS at its rank, a unit's record by popcount;
   // two 64-unit windows per step with both loads (random sources: the permuted records) and their
-  // wait in one asm statement.
+  // wait in one asm statement.  Against the shuffle-search form: sort + pack 14.2 -> 13.4 ms at
+  // 5 GB, the same order and payloads (profiles/r05/ab/sort_gather_5g_*.json).
   __shared__ uint4 s_rec[4][64];
   __shared__ uint32_t s_first[4][64];
   uint4* const recs = s_rec[threadIdx.x >> 6];
@@ -237,52 +230,6 @@ __global__ __launch_bounds__(256) void k_gather_records_tile(const uint8_t* __re
       }
     }
   }
-#else
-  for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); t < ntiles; t += wstride) {
-    const uint64_t i = t * 64 + lane;
-    uint64_t src = 0, dst = 0;
-    uint32_t len = 0;
-    if (i < n) {
-      src = rec_off[perm ? perm[i] : i];
-      dst = out_off[i];
-      len = (uint32_t)(out_off[i + 1] - dst);
-    }
-    const uint32_t units = (len + 15u) >> 4;
-    uint32_t incl = units;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t v = __shfl_up(incl, off);
-      if ((int)lane >= off) incl += v;
-    }
-    const uint32_t excl = incl - units;
-    const uint32_t total = __shfl(incl, 63);
-    for (uint32_t q0 = 0; q0 < total; q0 += 64) {
-      const uint32_t q = q0 + lane;
-      uint32_t lo = 0;
-#pragma unroll
-      for (uint32_t step = 32; step; step >>= 1) {
-        const uint32_t m = lo + step;
-        if (__shfl(excl, m) <= q) lo = m;
-      }
-      const uint32_t k = q - __shfl(excl, lo);
-      const uint32_t nb = __shfl(len, lo) - 16u * k;
-      const uint64_t sq = __shfl(src, lo), dq = __shfl(dst, lo);
-      if (q < total) {
-        const g_u32x4_a1 v = *(const g_u32x4_a1*)(ubuf + sq + 16u * k);
-        uint8_t* dp = out + dq + 16u * k;
-        if (nb >= 16u) {
-          *(g_u32x4_a1*)dp = v;
-        } else {
-          uint64_t lo8 = (uint64_t)v[0] | (uint64_t)v[1] << 32, hi8 = (uint64_t)v[2] | (uint64_t)v[3] << 32;
-          if (nb & 8u) { *(g_u64_a1*)dp = lo8; dp += 8; lo8 = hi8; }
-          if (nb & 4u) { *(g_u32_a1*)dp = (uint32_t)lo8; dp += 4; lo8 >>= 32; }
-          if (nb & 2u) { *(g_u16_a1*)dp = (uint16_t)lo8; dp += 2; lo8 >>= 16; }
-          if (nb & 1u) *dp = (uint8_t)lo8;
-        }
-      }
-    }
-  }
-#endif
 }
 
 // TotalOrderPartitioner bounds: for split point j, the first index whose (signed) key is
