@@ -84,11 +84,29 @@ __global__ __launch_bounds__(256) void k_scan_chunks(const uint8_t* __restrict__
   for (uint32_t step = 0; step < SCAN_CHUNK / (256 * SP); ++step) {
     const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * SP;
     if (p0 >= end) break;
-    // byte-aligned dword loads (the compiler merges them into wide loads): positions p0..p0+SP-1
-    // need bytes up to p0 + SP + 11
+    // positions p0..p0+SP-1 need bytes up to p0 + SP + 11
     uint32_t w[SP / 4 + 3];
+    // SP bytes per lane as 16-byte loads (a wave reads 2 KiB with no overlap), the 12 bytes after
+    // them from the next lane by DPP wave_shl:1 (lane 63: one extra load of its own); against
+    // SP/4 + 3 byte-aligned dword loads per lane (the last three overlapping the next lane's):
+    // 1.346 -> 1.241 ms at 5 GB (profiles/r05/ab/scan_dpp_neighbour_5g.txt)
+    static_assert(SP % 16 == 0, "scan: whole 16-byte loads per lane");
 #pragma unroll
-    for (int i = 0; i < SP / 4 + 3; ++i) w[i] = ld_u32_unaligned(comp + p0 + 4 * i);
+    for (int i = 0; i < SP / 16; ++i) {
+      const u32x4_t q = *(const __attribute__((address_space(1))) u32x4_t*)(comp + p0 + 16 * i);
+      w[4 * i] = q[0]; w[4 * i + 1] = q[1]; w[4 * i + 2] = q[2]; w[4 * i + 3] = q[3];
+    }
+    uint32_t x0 = 0, x1 = 0, x2 = 0;
+    if ((threadIdx.x & 63u) == 63u) {
+      x0 = ld_u32_unaligned(comp + p0 + SP);
+      x1 = ld_u32_unaligned(comp + p0 + SP + 4);
+      x2 = ld_u32_unaligned(comp + p0 + SP + 8);
+    }
+    // (a lane whose right neighbour has left the loop only needs neighbour bytes for positions
+    // past `end`, which are not tested)
+    w[SP / 4] = (uint32_t)__builtin_amdgcn_update_dpp((int)x0, (int)w[0], 0x130, 0xf, 0xf, false);
+    w[SP / 4 + 1] = (uint32_t)__builtin_amdgcn_update_dpp((int)x1, (int)w[1], 0x130, 0xf, 0xf, false);
+    w[SP / 4 + 2] = (uint32_t)__builtin_amdgcn_update_dpp((int)x2, (int)w[2], 0x130, 0xf, 0xf, false);
 #pragma unroll
     for (int k = 0; k < SP; ++k) {
       const uint64_t p = p0 + k;

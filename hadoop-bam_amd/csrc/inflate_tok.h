@@ -113,6 +113,32 @@ __device__ __forceinline__ void ein_refill(EIn& e) {
     --e.nv;
   }
 }
+#ifndef HBAM_TOK_BL
+#define HBAM_TOK_BL 0
+#endif
+// the same without a branch (the fast path: a branch around it costs every iteration the exec-mask
+// bookkeeping, since some lane of 64 nearly always needs the dword)
+__device__ __forceinline__ void ein_refill_sel(EIn& e) {
+  const bool need = e.bc <= 32u && e.nv != 0u;
+  const uint64_t add = (uint64_t)ein_sel(e, e.rd) << (e.bc & 63u);
+  e.bb |= need ? add : 0ull;
+  e.bc += need ? 32u : 0u;
+  e.rd = need ? ((e.rd + 1u) & 7u) : e.rd;
+  e.nv -= need ? 1u : 0u;
+}
+// length / distance bases without branches (DEFLATE tables as arithmetic; RFC 1951 3.2.5)
+__device__ __forceinline__ void length_base_sel(uint32_t sym, uint32_t& base, uint32_t& extra) {
+  const uint32_t i = sym - 257u;  // [0, 28]
+  const uint32_t ex = i < 8u ? 0u : ((i - 4u) >> 2);
+  const uint32_t b = i < 8u ? 3u + i : ((4u + (i & 3u)) << ex) + 3u;
+  extra = i < 28u ? ex : 0u;
+  base = i < 28u ? b : 258u;
+}
+__device__ __forceinline__ void dist_base_sel(uint32_t d, uint32_t& base, uint32_t& extra) {
+  const uint32_t ex = d < 4u ? 0u : (d >> 1) - 1u;
+  extra = ex;
+  base = d < 4u ? d + 1u : ((2u + (d & 1u)) << ex) + 1u;
+}
 // epoch boundary: merge the quad in flight into the free bank, request the next one
 __device__ __forceinline__ void ein_epoch_merge(EIn& e) {
   if (e.fp < e.fend && e.nv <= 4u) {
@@ -508,7 +534,11 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
                                                   const uint8_t* __restrict__ syms_ll,
                                                   const uint8_t* __restrict__ syms_d, TSink& sink,
                                                   uint32_t& op, uint32_t isize) {
+#if HBAM_TOK_BL
+  ein_refill_sel(in);
+#else
   ein_refill(in);
+#endif
   uint32_t L1, idx1, hi1 = 0, L2, idx2, hi2 = 0;
   const bool ok1 = huffp_lookup<true>(hl, ein_rev15(in), L1, idx1, hi1);
   const uint32_t l1 = ok1 ? L1 : 0u;
@@ -535,8 +565,13 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   ex = (ism && m > 285u) ? 3u : ex;
   const bool dom = ism && m > 256u && m <= 285u;
   uint32_t lbase, lext;
+#if HBAM_TOK_BL
+  length_base_sel(dom ? m : 257u, lbase, lext);
+  ein_refill_sel(in);
+#else
   length_base(dom ? m : 257u, lbase, lext);
   ein_refill(in);
+#endif
   lext = dom ? lext : 0u;
   const uint32_t mlen = lbase + ein_peek(in, lext);
   ein_drop(in, lext);
@@ -548,7 +583,11 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   ex = (dom && okd && dsym > 29u) ? 3u : ex;
   const bool dom2 = dom && ex == 0u;
   uint32_t dbase, dext;
+#if HBAM_TOK_BL
+  dist_base_sel(dom2 ? dsym : 0u, dbase, dext);
+#else
   dist_base(dom2 ? dsym : 0u, dbase, dext);
+#endif
   dext = dom2 ? dext : 0u;
   const uint32_t dist = dbase + ein_peek(in, dext);
   ein_drop(in, dext);
