@@ -113,11 +113,10 @@ __device__ __forceinline__ void ein_refill(EIn& e) {
     --e.nv;
   }
 }
-#ifndef HBAM_TOK_BL
-#define HBAM_TOK_BL 0
-#endif
 // the same without a branch (the fast path: a branch around it costs every iteration the exec-mask
-// bookkeeping, since some lane of 64 nearly always needs the dword)
+// bookkeeping, since some lane of 64 nearly always needs the dword).  With the branchless length /
+// distance bases below: Huffman 33.9 -> 32.1 ms at 5 GB, same output
+// (profiles/r05/ab/huffman_branchless_refill_bases_5g.txt)
 __device__ __forceinline__ void ein_refill_sel(EIn& e) {
   const bool need = e.bc <= 32u && e.nv != 0u;
   const uint64_t add = (uint64_t)ein_sel(e, e.rd) << (e.bc & 63u);
@@ -300,13 +299,17 @@ struct TSink {
   uint8_t* cbase;   // 16-aligned address of chunk 0 (the chunk holding the block's first byte)
   uint32_t soff;    // block start inside chunk 0
   uint32_t iend;    // soff + isize
-  uint32_t curc;    // chunk held in lo/hi (~0u = none)
+  uint32_t curc;    // chunk held in lo/hi (0 at the start: the block's first byte is in chunk 0)
   uint64_t lo, hi;
   uint32_t* bm;     // match-start bitmap of the block (BITMAP_WORDS words)
-  uint32_t bwin;    // 128-position window held in w0..w3
+  uint32_t bwin;    // 128-position window held in wl (positions 0-63) / wh (64-127)
   uint32_t nwin;    // windows covering the block
-  uint32_t w0, w1, w2, w3;
+  uint64_t wl, wh;
   uint32_t* tail;   // [0] = op | n<<16 | 1<<31 for a final match shorter than 3 bytes, [1] = dist
+  uint32_t t0, t1;  // tail[0..1], stored by finish() (a store behind a branch in the loop cost
+                    // every iteration its exec-mask bookkeeping; with the unconditional chunk 0
+                    // and the 64-bit bitmap words: Huffman 32.5 -> 31.0 ms at 5 GB, same output,
+                    // profiles/r05/ab/huffman_sink_tail_mark_5g.txt)
   uint8_t* edge;    // 32 B: the block's partial first / last 16-byte chunk (k_edge_merge)
 
   __device__ __forceinline__ void init(uint8_t* ubuf, uint64_t start, uint32_t isize, uint32_t* bmp,
@@ -315,17 +318,16 @@ struct TSink {
     cbase = ubuf + (start & ~15ull);
     soff = (uint32_t)(start & 15u);
     iend = soff + isize;
-    curc = ~0u;
+    curc = 0;  // (a flush before any output writes zeros to the block's own chunk 0 / edge slot)
     lo = hi = 0;
     bm = bmp;
     bwin = 0;
     nwin = (isize + 127u) >> 7;
-    w0 = w1 = w2 = w3 = 0;
+    wl = wh = 0;
     tail = tl;
-    tail[0] = 0;
+    t0 = t1 = 0;
   }
   __device__ __forceinline__ void flush() {
-    if (curc == ~0u) return;
     const uint32_t r0 = curc << 4;
     // A chunk shared with a neighbouring block (the block's first chunk when it does not
     // start 16-aligned, its last when it does not end so) goes to the block's edge slot
@@ -344,20 +346,20 @@ struct TSink {
     }
   }
   __device__ __forceinline__ void win_store() {
-    st_out((uint4*)(bm + 4u * bwin), make_uint4(w0, w1, w2, w3));
+    st_out((uint4*)(bm + 4u * bwin),
+           make_uint4((uint32_t)wl, (uint32_t)(wl >> 32), (uint32_t)wh, (uint32_t)(wh >> 32)));
   }
   __device__ __forceinline__ void mark(uint32_t op) {
     const uint32_t w = op >> 7;
     while (bwin < w) {
       win_store();
-      w0 = w1 = w2 = w3 = 0;
+      wl = wh = 0;
       ++bwin;
     }
-    const uint32_t i = op & 127u, m = 1u << (i & 31u), q = i >> 5;
-    w0 |= q == 0u ? m : 0u;
-    w1 |= q == 1u ? m : 0u;
-    w2 |= q == 2u ? m : 0u;
-    w3 |= q == 3u ? m : 0u;
+    const uint32_t i = op & 127u;
+    const uint64_t m = 1ull << (i & 63u);  // one 64-bit shift and two selects (was four compares)
+    wl |= i < 64u ? m : 0ull;
+    wh |= i < 64u ? 0ull : m;
   }
   __device__ __forceinline__ void literal(uint32_t op, uint32_t b) {
     const uint32_t r = soff + op;
@@ -368,8 +370,8 @@ struct TSink {
   }
   __device__ __forceinline__ void match(uint32_t op, uint32_t n, uint32_t dist) {
     if (n < 3u) {  // the output filled up inside the match: last token of the block
-      tail[0] = op | n << 16 | 0x80000000u;
-      tail[1] = dist;
+      t0 = op | n << 16 | 0x80000000u;
+      t1 = dist;
       return;
     }
     const uint64_t d = (uint64_t)((n - 3u) | (dist - 1u) << 8);  // 3 bytes
@@ -421,9 +423,11 @@ struct TSink {
   }
   __device__ __forceinline__ void finish() {
     flush();
+    tail[0] = t0;
+    tail[1] = t1;
     while (bwin < nwin) {
       win_store();
-      w0 = w1 = w2 = w3 = 0;
+      wl = wh = 0;
       ++bwin;
     }
   }
@@ -534,11 +538,7 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
                                                   const uint8_t* __restrict__ syms_ll,
                                                   const uint8_t* __restrict__ syms_d, TSink& sink,
                                                   uint32_t& op, uint32_t isize) {
-#if HBAM_TOK_BL
   ein_refill_sel(in);
-#else
-  ein_refill(in);
-#endif
   uint32_t L1, idx1, hi1 = 0, L2, idx2, hi2 = 0;
   const bool ok1 = huffp_lookup<true>(hl, ein_rev15(in), L1, idx1, hi1);
   const uint32_t l1 = ok1 ? L1 : 0u;
@@ -565,13 +565,8 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   ex = (ism && m > 285u) ? 3u : ex;
   const bool dom = ism && m > 256u && m <= 285u;
   uint32_t lbase, lext;
-#if HBAM_TOK_BL
   length_base_sel(dom ? m : 257u, lbase, lext);
   ein_refill_sel(in);
-#else
-  length_base(dom ? m : 257u, lbase, lext);
-  ein_refill(in);
-#endif
   lext = dom ? lext : 0u;
   const uint32_t mlen = lbase + ein_peek(in, lext);
   ein_drop(in, lext);
@@ -583,11 +578,7 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   ex = (dom && okd && dsym > 29u) ? 3u : ex;
   const bool dom2 = dom && ex == 0u;
   uint32_t dbase, dext;
-#if HBAM_TOK_BL
   dist_base_sel(dom2 ? dsym : 0u, dbase, dext);
-#else
-  dist_base(dom2 ? dsym : 0u, dbase, dext);
-#endif
   dext = dom2 ? dext : 0u;
   const uint32_t dist = dbase + ein_peek(in, dext);
   ein_drop(in, dext);
@@ -596,10 +587,9 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   const bool domatch = dom2 && ex == 0u;
   uint32_t n = isize - op;
   n = mlen < n ? mlen : n;
-  if (domatch && n < 3u) {  // the output filled up inside the match: last token of the block
-    sink.tail[0] = op | n << 16 | 0x80000000u;
-    sink.tail[1] = dist;
-  }
+  const bool last = domatch && n < 3u;  // the output filled up inside the match: last token
+  sink.t0 = last ? (op | n << 16 | 0x80000000u) : sink.t0;
+  sink.t1 = last ? dist : sink.t1;
   const bool em = domatch && n >= 3u;
   uint64_t P = emit1 ? (uint64_t)(sym1 & 0xffu) : 0ull;
   P |= emit2 ? (uint64_t)(sym2 & 0xffu) << 8 : 0ull;
