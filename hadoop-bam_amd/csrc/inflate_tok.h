@@ -126,17 +126,19 @@ __device__ __forceinline__ void ein_refill_sel(EIn& e) {
   e.nv -= need ? 1u : 0u;
 }
 // length / distance bases without branches (DEFLATE tables as arithmetic; RFC 1951 3.2.5)
+// (one formula for every code, the exceptions as constant selects: written as a select between
+// two computed arms, the compiler turned the length base back into a branch)
 __device__ __forceinline__ void length_base_sel(uint32_t sym, uint32_t& base, uint32_t& extra) {
   const uint32_t i = sym - 257u;  // [0, 28]
-  const uint32_t ex = i < 8u ? 0u : ((i - 4u) >> 2);
-  const uint32_t b = i < 8u ? 3u + i : ((4u + (i & 3u)) << ex) + 3u;
+  const uint32_t ex = ((i > 4u ? i : 4u) - 4u) >> 2;  // 0 for codes 257-264
+  const uint32_t b = ((4u + (i & 3u)) << ex) + 3u - (i < 4u ? 4u : 0u);
   extra = i < 28u ? ex : 0u;
   base = i < 28u ? b : 258u;
 }
 __device__ __forceinline__ void dist_base_sel(uint32_t d, uint32_t& base, uint32_t& extra) {
-  const uint32_t ex = d < 4u ? 0u : (d >> 1) - 1u;
+  const uint32_t ex = ((d > 2u ? d : 2u) >> 1) - 1u;  // 0 for codes 0-3
   extra = ex;
-  base = d < 4u ? d + 1u : ((2u + (d & 1u)) << ex) + 1u;
+  base = ((2u + (d & 1u)) << ex) + 1u - (d < 2u ? 2u : 0u);
 }
 // epoch boundary: merge the quad in flight into the free bank, request the next one
 __device__ __forceinline__ void ein_epoch_merge(EIn& e) {
@@ -349,17 +351,23 @@ struct TSink {
     st_out((uint4*)(bm + 4u * bwin),
            make_uint4((uint32_t)wl, (uint32_t)(wl >> 32), (uint32_t)wh, (uint32_t)(wh >> 32)));
   }
-  __device__ __forceinline__ void mark(uint32_t op) {
+  __device__ __forceinline__ void mark(uint32_t op) { mark_if(true, op); }
+  // the match-start bit of op when em: the bit as selects, only the window store behind a branch
+  __device__ __forceinline__ void mark_if(bool em, uint32_t op) {
     const uint32_t w = op >> 7;
-    while (bwin < w) {
+    if (em && bwin < w) {
       win_store();
       wl = wh = 0;
       ++bwin;
+      while (bwin < w) {  // a match longer than the window: zero windows
+        win_store();
+        ++bwin;
+      }
     }
     const uint32_t i = op & 127u;
     const uint64_t m = 1ull << (i & 63u);  // one 64-bit shift and two selects (was four compares)
-    wl |= i < 64u ? m : 0ull;
-    wh |= i < 64u ? 0ull : m;
+    wl |= (em && i < 64u) ? m : 0ull;
+    wh |= (em && i >= 64u) ? m : 0ull;
   }
   __device__ __forceinline__ void literal(uint32_t op, uint32_t b) {
     const uint32_t r = soff + op;
@@ -596,7 +604,7 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   const uint32_t nl = (emit1 ? 1u : 0u) + (emit2 ? 1u : 0u);
   P |= em ? (uint64_t)((n - 3u) | (dist - 1u) << 8) << (8u * nl) : 0ull;
   sink.put(op1, P, nl + (em ? 3u : 0u));
-  if (em) sink.mark(op);
+  sink.mark_if(em, op);
   op += domatch ? n : 0u;
   ex = (domatch && n < mlen) ? 2u : ex;
   return ex;
@@ -807,21 +815,25 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
     TOK_PT(6);  // header + tables
     {
       uint32_t ex = 0;  // 0 next symbol, 1 end of block, 2 leave (zlib stops), 3 data error
-      do {
+      // A wave-uniform loop (the exit is a ballot): a lane whose block has ended idles in it, as
+      // it idled at the exit of a divergent loop, without the per-iteration exec-mask bookkeeping
+      // of one.  The careful symbol (a lane's last 64 stream bits) runs behind a wave-uniform test.
+      // With the predicated match mark and the branch-free bases: Huffman 31.1 -> 30.65 ms at
+      // 5 GB, same output (profiles/r05/ab/huffman_uniform_loop_5g.txt).
+      for (;;) {
         TOK_PC(0);
-        // epoch clock: the first active lane's, so the branch is scalar and every active lane
-        // merges / requests its quad at the same iteration
         if ((__builtin_amdgcn_readfirstlane(++it) & (TOK_K - 1u)) == 0u) ein_epoch(in);
-        if (!ein_short(in, TOK_FAST_BITS)) {  // else stall until the next epoch merges more input
-          if (in.total - in.consumed >= TOK_FAST_BITS)
-            ex = tok_fast_spec(in, hl, hd, syms_ll, syms_d, sink, op, isize);
-          else
-            ex = tok_careful(in, hl, hd, syms_ll, syms_d, sink, op, isize);
+        const bool run = ex == 0u && !ein_short(in, TOK_FAST_BITS);
+        const bool fast = in.total - in.consumed >= TOK_FAST_BITS;
+        if (run && fast) ex = tok_fast_spec(in, hl, hd, syms_ll, syms_d, sink, op, isize);
+        if (__builtin_amdgcn_ballot_w64(run && !fast) != 0u) {
+          if (run && !fast) ex = tok_careful(in, hl, hd, syms_ll, syms_d, sink, op, isize);
         }
 #ifdef HBAM_PROF
         TOK_PT(1);
 #endif
-      } while (ex == 0u);
+        if (__builtin_amdgcn_ballot_w64(ex == 0u) == 0u) break;
+      }
       if (ex == 2u) goto leave;
       if (ex == 3u) {
         rc = INF_DATA;

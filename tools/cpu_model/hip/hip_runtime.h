@@ -24,5 +24,6 @@ static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
 
 // one lane: the first active lane is this lane; waits and clocks are no-ops
 #define __builtin_amdgcn_readfirstlane(x) (x)
+#define __builtin_amdgcn_ballot_w64(x) ((uint64_t)((x) ? 1u : 0u))
 #define __builtin_amdgcn_s_waitcnt(x) ((void)0)
 #define __builtin_amdgcn_s_memtime() ((uint64_t)0)
