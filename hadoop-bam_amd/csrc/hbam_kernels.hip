@@ -881,10 +881,135 @@ static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
   return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l) << 32;
 }
+// Record-major units (HBAM_POOLS_RM): the field-major loop below reads a tile's source lines once
+// per field, and a tile's source (64 records, ~22 KB) is evicted from the 4 MB L2 of an XCD (768
+// resident waves) before the next field comes to it — FETCH_SIZE counted 2.8 x U for that loop
+// (profiles/r05/pmc_kernels.json).  Here a tile's segments (record, field) are numbered in record
+// order, so the windows walk the tile's source once, front to back, and are full across field
+// ends.  A unit finds its segment as before (the segment starts in its window are one bit each of
+// a mask, the earlier ones counted by ballots — five per window, a segment per field per lane);
+// one ds_read_b128 per unit gives (source, destination, field | length, first unit).  Taken for
+// tiles whose fields are all < 16 MiB (field id in the length's top bits, unit counts < 2^32);
+// other tiles take the field-major loop.
+#ifndef HBAM_POOLS_RM
+#define HBAM_POOLS_RM 1
+#endif
+#if HBAM_POOLS_RM
+static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__ u, const DevColumns& c,
+                                                     uint4* segs, uint32_t lane, uint64_t le, uint64_t src,
+                                                     const uint32_t (&L)[5], const uint64_t (&d)[5]) {
+  uint32_t so[5], uf[5];
+  so[0] = 0u;
+  so[1] = L[0];
+  so[2] = so[1] + L[1];
+  so[3] = so[2] + (L[2] + 1u) / 2u;  // packed SEQ
+  so[4] = so[3] + L[3];
+  uint32_t R = 0u, ne = 0u;
+#pragma unroll
+  for (int f = 0; f < 5; ++f) {
+    uf[f] = (L[f] + 15u) >> 4;
+    R += uf[f];
+    ne += uf[f] != 0u ? 1u : 0u;
+  }
+  const uint32_t incl = wave_scan_dpp(R), E = incl - R, T = wave_last(incl);
+  if (T == 0u) return;
+  const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(R != 0u));
+  const uint64_t sb = readlane64(src, first);
+  uint64_t db[5];
+#pragma unroll
+  for (int f = 0; f < 5; ++f) db[f] = readlane64(d[f], first);
+  const uint32_t sr = wave_scan_dpp(ne) - ne;
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");  // the previous tile's reads of segs precede these writes
+  uint32_t st[5], k = sr, cum = E;
+#pragma unroll
+  for (int f = 0; f < 5; ++f) {
+    st[f] = ~0u;  // an empty segment: never before a window, never inside one
+    if (uf[f] != 0u) {
+      segs[k++] = make_uint4((uint32_t)(src - sb) + so[f], (uint32_t)(d[f] - db[f]), L[f] | (uint32_t)f << 29, cum);
+      st[f] = cum;
+    }
+    cum += uf[f];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  uint8_t* const pb0 = c.names + db[0];
+  uint8_t* const pb1 = (uint8_t*)c.cigars + db[1];
+  uint8_t* const pb2 = c.seq + db[2];
+  uint8_t* const pb3 = c.qual + db[3];
+  uint8_t* const pb4 = c.aux + db[4];
+  const uint8_t* const sbase = u + sb;
+  for (uint32_t q0 = 0; q0 < T; q0 += 64 * HBAM_POOLS_U) {
+    u32x4_t raw[HBAM_POOLS_U];
+    const uint8_t* sp[HBAM_POOLS_U];
+    uint8_t* dp[HBAM_POOLS_U];
+    uint32_t nn[HBAM_POOLS_U], fs[HBAM_POOLS_U];
+#pragma unroll
+    for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
+      nn[w] = 0;
+      fs[w] = 0;
+      dp[w] = pb0;
+      sp[w] = sbase;
+      const uint32_t qw = q0 + 64u * w;
+      if (qw >= T) continue;  // wave-uniform
+      const uint32_t q = qw + lane;
+      uint32_t blo = 0u, bhi = 0u, c0 = 0u;
+#pragma unroll
+      for (int f = 0; f < 5; ++f) {
+        const uint32_t pos = st[f] - qw;
+        const bool in = st[f] >= qw && pos < 64u;
+        blo |= (in && pos < 32u) ? 1u << (pos & 31u) : 0u;
+        bhi |= (in && pos >= 32u) ? 1u << (pos & 31u) : 0u;
+        c0 += (uint32_t)__popcll(__ballot(st[f] < qw));
+      }
+      const uint64_t M = (uint64_t)wave_last(wave_scan_dpp(bhi)) << 32 | wave_last(wave_scan_dpp(blo));
+      if (q < T) {
+        const uint4 rr = segs[c0 + (uint32_t)__popcll(M & le) - 1u];
+        const uint32_t f = rr.z >> 29, j = q - rr.w;
+        nn[w] = (rr.z & 0x1fffffffu) - 16u * j;
+        uint8_t* const pb = f == 0u ? pb0 : f == 1u ? pb1 : f == 2u ? pb2 : f == 3u ? pb3 : pb4;
+        dp[w] = pb + rr.y + 16u * j;
+        sp[w] = sbase + rr.x + (f == 2u ? 8u : 16u) * j;
+        fs[w] = f;
+      }
+    }
+#if HBAM_POOLS_U == 2
+    asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off\n\ts_waitcnt vmcnt(0)"
+                 : "=&v"(raw[0]), "=&v"(raw[1]) : "v"(sp[0]), "v"(sp[1]) : "memory");
+#elif HBAM_POOLS_U == 3
+    asm volatile("global_load_dwordx4 %0, %3, off\n\tglobal_load_dwordx4 %1, %4, off\n\t"
+                 "global_load_dwordx4 %2, %5, off\n\ts_waitcnt vmcnt(0)"
+                 : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]) : "v"(sp[0]), "v"(sp[1]), "v"(sp[2]) : "memory");
+#else
+    asm volatile("global_load_dwordx4 %0, %4, off\n\tglobal_load_dwordx4 %1, %5, off\n\t"
+                 "global_load_dwordx4 %2, %6, off\n\tglobal_load_dwordx4 %3, %7, off\n\ts_waitcnt vmcnt(0)"
+                 : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]), "=&v"(raw[3])
+                 : "v"(sp[0]), "v"(sp[1]), "v"(sp[2]), "v"(sp[3]) : "memory");
+#endif
+#pragma unroll
+    for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
+      if (q0 + 64u * w >= T) break;  // wave-uniform
+      u32x4_a1 v = u32x4_a1{raw[w][0], raw[w][1], raw[w][2], raw[w][3]};
+      if (__ballot(fs[w] == 2u) != 0ull) {  // a SEQ unit in the window: 8 packed bytes -> 16 chars
+        const uint64_t qq = (uint64_t)raw[w][0] | (uint64_t)raw[w][1] << 32;
+        const bool sq = fs[w] == 2u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t x = seq4((uint32_t)(qq >> (16 * j)) & 0xffu, (uint32_t)(qq >> (16 * j + 8)) & 0xffu);
+          v[j] = sq ? x : v[j];
+        }
+      }
+      HBAM_G uint8_t* const gd = (HBAM_G uint8_t*)dp[w];
+      if (nn[w] >= 16u) *(HBAM_G u32x4_a1*)gd = v;
+      else if (nn[w] != 0u) st_part_g(gd, nn[w], v);
+    }
+  }
+}
+#endif
 __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict__ u, uint64_t nrec,
                                                        const uint64_t* __restrict__ rec_off,
                                                        DevColumns c) {
-  __shared__ uint4 s_recs[4][64];
+  __shared__ uint4 s_recs[4][HBAM_POOLS_RM ? 320 : 64];
   const uint32_t lane = threadIdx.x & 63u;
   uint4* const recs = s_recs[threadIdx.x >> 6];
   const uint64_t ntiles = (nrec + 63) / 64;
@@ -905,6 +1030,17 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
       o_seq = c.seq_off[r];
       o_aux = c.aux_off[r];
     }
+#if HBAM_POOLS_RM
+    {
+      const uint32_t L[5] = {nl, 4u * nc, ls, ls, na};
+      const uint64_t d[5] = {o_name, 4 * o_cig, o_seq, o_seq, o_aux};
+      const uint32_t mx = max(max(max(L[0], L[1]), max(L[2], L[4])), 0u);
+      if (__ballot(mx >= (1u << 24)) == 0ull) {  // wave-uniform
+        pools_tile_rm(u, c, recs, lane, le, src, L, d);
+        continue;
+      }
+    }
+#endif
 #pragma unroll 1
     for (uint32_t f = 0; f < 5; ++f) {
       uint32_t len;
