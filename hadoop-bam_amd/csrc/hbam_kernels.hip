@@ -919,6 +919,9 @@ static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
 #ifndef HBAM_POOLS_RM
 #define HBAM_POOLS_RM 1
 #endif
+#ifndef HBAM_POOLS_BACK
+#define HBAM_POOLS_BACK 1
+#endif
 #if HBAM_POOLS_RM
 static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__ u, const DevColumns& c,
                                                      uint4* segs, uint32_t lane, uint64_t le, uint64_t src,
@@ -990,11 +993,21 @@ static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__
       const uint64_t M = (uint64_t)wave_last(wave_scan_dpp(bhi)) << 32 | wave_last(wave_scan_dpp(blo));
       if (q < T) {
         const uint4 rr = segs[c0 + (uint32_t)__popcll(M & le) - 1u];
-        const uint32_t f = rr.z >> 29, j = q - rr.w;
-        nn[w] = (rr.z & 0x1fffffffu) - 16u * j;
+        const uint32_t f = rr.z >> 29, j = q - rr.w, len = rr.z & 0x1fffffffu;
+        uint32_t n = len - 16u * j;
         uint8_t* const pb = f == 0u ? pb0 : f == 1u ? pb1 : f == 2u ? pb2 : f == 3u ? pb3 : pb4;
-        dp[w] = pb + rr.y + 16u * j;
-        sp[w] = sbase + rr.x + (f == 2u ? 8u : 16u) * j;
+#if HBAM_POOLS_BACK
+        // a segment's last, partial unit of a segment >= 16 bytes as the segment's last 16 bytes
+        // (a whole store; the bytes it repeats are the previous unit's, written with the same
+        // values); SEQ only when the shift is whole packed bytes
+        const uint32_t sb = (n < 16u && len >= 16u && (f != 2u || (n & 1u) == 0u)) ? 16u - n : 0u;
+        n += sb;
+#else
+        const uint32_t sb = 0u;
+#endif
+        nn[w] = n;
+        dp[w] = pb + rr.y + 16u * j - sb;
+        sp[w] = sbase + rr.x + (f == 2u ? 8u * j - sb / 2u : 16u * j - sb);
         fs[w] = f;
       }
     }
