@@ -911,11 +911,13 @@ static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
 // resident waves) before the next field comes to it — FETCH_SIZE counted 2.8 x U for that loop
 // (profiles/r05/pmc_kernels.json).  Here a tile's segments (record, field) are numbered in record
 // order, so the windows walk the tile's source once, front to back, and are full across field
-// ends.  A unit finds its segment as before (the segment starts in its window are one bit each of
-// a mask, the earlier ones counted by ballots — five per window, a segment per field per lane);
-// one ds_read_b128 per unit gives (source, destination, field | length, first unit).  Taken for
-// tiles whose fields are all < 16 MiB (field id in the length's top bits, unit counts < 2^32);
-// other tiles take the field-major loop.
+// ends.  A unit's segment is found in two steps: its record by the record starts' mask (one bit
+// per lane, two DPP scans and a ballot per window, as the field-major loop), then its field by
+// the record's cumulative unit counts (16-bit, in the record's LDS entry), the segment's entry at
+// 64 + 5 x record + field; the five pool bases come from a per-wave LDS table.  (A first form
+// found the segment directly, five segment starts per lane in the window mask: 0.3-0.5 ms slower
+// at 5 GB, profiles/r05/ab/pools_record_level_mapping_5g.txt.)  Taken for tiles whose records
+// are all under 2^16 units (1 MiB); other tiles take the field-major loop.
 #ifndef HBAM_POOLS_RM
 #define HBAM_POOLS_RM 1
 #endif
@@ -924,48 +926,43 @@ static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
 #endif
 #if HBAM_POOLS_RM
 static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__ u, const DevColumns& c,
-                                                     uint4* segs, uint32_t lane, uint64_t le, uint64_t src,
-                                                     const uint32_t (&L)[5], const uint64_t (&d)[5]) {
-  uint32_t so[5], uf[5];
+                                                      uint4* segs, uint64_t* pbt, uint32_t lane, uint64_t le,
+                                                      uint64_t src, const uint32_t (&L)[5],
+                                                      const uint64_t (&d)[5], uint32_t R) {
+  uint32_t so[5], cu[5];
   so[0] = 0u;
   so[1] = L[0];
   so[2] = so[1] + L[1];
   so[3] = so[2] + (L[2] + 1u) / 2u;  // packed SEQ
   so[4] = so[3] + L[3];
-  uint32_t R = 0u, ne = 0u;
+  cu[0] = 0u;
 #pragma unroll
-  for (int f = 0; f < 5; ++f) {
-    uf[f] = (L[f] + 15u) >> 4;
-    R += uf[f];
-    ne += uf[f] != 0u ? 1u : 0u;
-  }
+  for (int f = 1; f < 5; ++f) cu[f] = cu[f - 1] + ((L[f - 1] + 15u) >> 4);
   const uint32_t incl = wave_scan_dpp(R), E = incl - R, T = wave_last(incl);
   if (T == 0u) return;
-  const uint32_t first = (uint32_t)__builtin_ctzll(__ballot(R != 0u));
+  const uint64_t mh = __ballot(R != 0u);
+  const uint32_t first = (uint32_t)__builtin_ctzll(mh);
   const uint64_t sb = readlane64(src, first);
   uint64_t db[5];
 #pragma unroll
   for (int f = 0; f < 5; ++f) db[f] = readlane64(d[f], first);
-  const uint32_t sr = wave_scan_dpp(ne) - ne;
   __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");  // the previous tile's reads of segs precede these writes
-  uint32_t st[5], k = sr, cum = E;
+  asm volatile("" ::: "memory");  // the previous tile's reads of segs / pbt precede these writes
+  if (R != 0u) {
+    const uint32_t rk = lane_rank(mh);
+    segs[rk] = make_uint4(E, (uint32_t)(src - sb), cu[1] | cu[2] << 16, cu[3] | cu[4] << 16);
 #pragma unroll
-  for (int f = 0; f < 5; ++f) {
-    st[f] = ~0u;  // an empty segment: never before a window, never inside one
-    if (uf[f] != 0u) {
-      segs[k++] = make_uint4((uint32_t)(src - sb) + so[f], (uint32_t)(d[f] - db[f]), L[f] | (uint32_t)f << 29, cum);
-      st[f] = cum;
-    }
-    cum += uf[f];
+    for (int f = 0; f < 5; ++f)
+      segs[64u + 5u * rk + (uint32_t)f] = make_uint4((uint32_t)(d[f] - db[f]), L[f], so[f], cu[f]);
+  }
+  if (lane < 5u) {
+    uint8_t* const b = lane == 0u ? c.names : lane == 1u ? (uint8_t*)c.cigars : lane == 2u ? c.seq
+                     : lane == 3u ? c.qual : c.aux;
+    const uint64_t dbl = lane == 0u ? db[0] : lane == 1u ? db[1] : lane == 2u ? db[2] : lane == 3u ? db[3] : db[4];
+    pbt[lane] = (uint64_t)(uintptr_t)(b + dbl);
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
-  uint8_t* const pb0 = c.names + db[0];
-  uint8_t* const pb1 = (uint8_t*)c.cigars + db[1];
-  uint8_t* const pb2 = c.seq + db[2];
-  uint8_t* const pb3 = c.qual + db[3];
-  uint8_t* const pb4 = c.aux + db[4];
   const uint8_t* const sbase = u + sb;
   for (uint32_t q0 = 0; q0 < T; q0 += 64 * HBAM_POOLS_U) {
     u32x4_t raw[HBAM_POOLS_U];
@@ -976,38 +973,35 @@ static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__
     for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
       nn[w] = 0;
       fs[w] = 0;
-      dp[w] = pb0;
+      dp[w] = (uint8_t*)sbase;  // (never stored through: nn = 0)
       sp[w] = sbase;
       const uint32_t qw = q0 + 64u * w;
       if (qw >= T) continue;  // wave-uniform
       const uint32_t q = qw + lane;
-      uint32_t blo = 0u, bhi = 0u, c0 = 0u;
-#pragma unroll
-      for (int f = 0; f < 5; ++f) {
-        const uint32_t pos = st[f] - qw;
-        const bool in = st[f] >= qw && pos < 64u;
-        blo |= (in && pos < 32u) ? 1u << (pos & 31u) : 0u;
-        bhi |= (in && pos >= 32u) ? 1u << (pos & 31u) : 0u;
-        c0 += (uint32_t)__popcll(__ballot(st[f] < qw));
-      }
+      const uint32_t pos = E - qw;
+      const bool inwin = R != 0u && E >= qw && pos < 64u;
+      const uint32_t blo = (inwin && pos < 32u) ? 1u << pos : 0u;
+      const uint32_t bhi = (inwin && pos >= 32u) ? 1u << (pos - 32u) : 0u;
       const uint64_t M = (uint64_t)wave_last(wave_scan_dpp(bhi)) << 32 | wave_last(wave_scan_dpp(blo));
+      const uint32_t c0 = (uint32_t)__popcll(__ballot(R != 0u && E < qw));
       if (q < T) {
-        const uint4 rr = segs[c0 + (uint32_t)__popcll(M & le) - 1u];
-        const uint32_t f = rr.z >> 29, j = q - rr.w, len = rr.z & 0x1fffffffu;
+        const uint32_t rk = c0 + (uint32_t)__popcll(M & le) - 1u;
+        const uint4 A = segs[rk];
+        const uint32_t dq = q - A.x;
+        const uint32_t f = (dq >= (A.z & 0xffffu) ? 1u : 0u) + (dq >= (A.z >> 16) ? 1u : 0u) +
+                           (dq >= (A.w & 0xffffu) ? 1u : 0u) + (dq >= (A.w >> 16) ? 1u : 0u);
+        const uint4 S = segs[64u + 5u * rk + f];
+        const uint32_t j = dq - S.w, len = S.y;
         uint32_t n = len - 16u * j;
-        uint8_t* const pb = f == 0u ? pb0 : f == 1u ? pb1 : f == 2u ? pb2 : f == 3u ? pb3 : pb4;
 #if HBAM_POOLS_BACK
-        // a segment's last, partial unit of a segment >= 16 bytes as the segment's last 16 bytes
-        // (a whole store; the bytes it repeats are the previous unit's, written with the same
-        // values); SEQ only when the shift is whole packed bytes
-        const uint32_t sb = (n < 16u && len >= 16u && (f != 2u || (n & 1u) == 0u)) ? 16u - n : 0u;
-        n += sb;
+        const uint32_t sbk = (n < 16u && len >= 16u && (f != 2u || (n & 1u) == 0u)) ? 16u - n : 0u;
+        n += sbk;
 #else
-        const uint32_t sb = 0u;
+        const uint32_t sbk = 0u;
 #endif
         nn[w] = n;
-        dp[w] = pb + rr.y + 16u * j - sb;
-        sp[w] = sbase + rr.x + (f == 2u ? 8u * j - sb / 2u : 16u * j - sb);
+        dp[w] = (uint8_t*)(uintptr_t)pbt[f] + S.x + 16u * j - sbk;
+        sp[w] = sbase + A.y + S.z + (f == 2u ? 8u * j - sbk / 2u : 16u * j - sbk);
         fs[w] = f;
       }
     }
@@ -1032,9 +1026,9 @@ static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__
         const uint64_t qq = (uint64_t)raw[w][0] | (uint64_t)raw[w][1] << 32;
         const bool sq = fs[w] == 2u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t x = seq4((uint32_t)(qq >> (16 * j)) & 0xffu, (uint32_t)(qq >> (16 * j + 8)) & 0xffu);
-          v[j] = sq ? x : v[j];
+        for (int jj = 0; jj < 4; ++jj) {
+          const uint32_t x = seq4((uint32_t)(qq >> (16 * jj)) & 0xffu, (uint32_t)(qq >> (16 * jj + 8)) & 0xffu);
+          v[jj] = sq ? x : v[jj];
         }
       }
       HBAM_G uint8_t* const gd = (HBAM_G uint8_t*)dp[w];
@@ -1047,7 +1041,10 @@ static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__
 __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict__ u, uint64_t nrec,
                                                        const uint64_t* __restrict__ rec_off,
                                                        DevColumns c) {
-  __shared__ uint4 s_recs[4][HBAM_POOLS_RM ? 320 : 64];
+  __shared__ uint4 s_recs[4][HBAM_POOLS_RM ? 384 : 64];
+#if HBAM_POOLS_RM
+  __shared__ uint64_t s_pb[4][8];
+#endif
   const uint32_t lane = threadIdx.x & 63u;
   uint4* const recs = s_recs[threadIdx.x >> 6];
   const uint64_t ntiles = (nrec + 63) / 64;
@@ -1072,9 +1069,15 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
     {
       const uint32_t L[5] = {nl, 4u * nc, ls, ls, na};
       const uint64_t d[5] = {o_name, 4 * o_cig, o_seq, o_seq, o_aux};
-      const uint32_t mx = max(max(max(L[0], L[1]), max(L[2], L[4])), 0u);
-      if (__ballot(mx >= (1u << 24)) == 0ull) {  // wave-uniform
-        pools_tile_rm(u, c, recs, lane, le, src, L, d);
+      uint32_t R = 0u;
+      bool big = false;
+#pragma unroll
+      for (int f = 0; f < 5; ++f) {
+        R += (L[f] + 15u) >> 4;
+        big |= L[f] >= (1u << 20);
+      }
+      if (__ballot(big || R >= (1u << 16)) == 0ull) {  // wave-uniform
+        pools_tile_rm(u, c, recs, s_pb[threadIdx.x >> 6], lane, le, src, L, d, R);
         continue;
       }
     }
