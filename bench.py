@@ -221,6 +221,62 @@ def parity_at_size(ctx, buf, dbuf, n_splits, seed, threads, whole=None):
     return out
 
 
+WHOLE_CHECK_GROUP = 4  # ranks holding a whole-launch host copy at once (N > 1)
+
+
+def host_views(hc):
+    """numpy views (no copy) of a host hbam_columns, keyed as _lib.host_columns_to_numpy"""
+    from hadoop_bam import _lib
+    n = int(hc.n_records)
+    out = {"n": n, "status": int(hc.status), "err_record": int(hc.err_record)}
+
+    def view(p, cnt, dt):
+        if not cnt or not p:
+            return np.zeros(cnt if p else 0, dt)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(cnt,))
+    for name, dt in _lib.FIXED:
+        out[name] = view(getattr(hc, name), n, dt)
+    for name in ("name_off", "cigar_off", "seq_off", "aux_off"):
+        out[name] = view(getattr(hc, name), n + 1, np.uint64)
+    out["ubuf"] = view(hc.ubuf, int(hc.ubuf_len), np.uint8)
+    for name, dt, off in (("names", np.uint8, "name_off"), ("cigars", np.uint32, "cigar_off"),
+                          ("seq", np.uint8, "seq_off"), ("qual", np.uint8, "seq_off"),
+                          ("aux", np.uint8, "aux_off")):
+        out[name] = view(getattr(hc, name), int(out[off][-1]) if n else 0, dt)
+    return out
+
+
+def whole_shard_check(ctx, cols, buf, own_len, off, threads):
+    """Every record of the timed launch (its host copy: columns, pools, record bytes) against the
+    oracle's BAMRecordReader over the same FileVirtualSplit, cut into FileSplits read in parallel
+    (oracle.check_whole, C).  Returns (result dict, the host copy to free, or None)."""
+    import oracle
+    from hadoop_bam import _lib
+    t = time.time()
+    hc = _lib.Columns()
+    if ctx.L.hbam_columns_to_host(ctx.h, C.byref(cols), C.byref(hc)):
+        return {"error": "hbam_columns_to_host: %s" % ctx.last_error()}, None
+    t_copy = time.time() - t
+    try:
+        d = oracle.OrDevCols()
+        d.n = int(hc.n_records)
+        d.voff_base = off << 16
+        d.ubuf_len = int(hc.ubuf_len)
+        for name, _ in oracle.OrDevCols._fields_:
+            if name not in ("n", "voff_base", "ubuf_len"):
+                setattr(d, name, C.cast(getattr(hc, name), C.c_void_p).value)
+        res = oracle.check_whole(np.ascontiguousarray(buf), own_len, N_REF, d, off << 16, 4 * threads, threads)
+    except Exception as e:  # reported, never hidden
+        res = {"error": "%s: %s" % (type(e).__name__, e)}
+    res["host_copy_s"] = round(t_copy, 2)
+    res["seconds"] = round(time.time() - t, 2)
+    res["what"] = ("every record of the timed launch (host copy of its output) vs the oracle's "
+                   "BAMRecordReader over the same split, cut into FileSplits aligned by the oracle's "
+                   "guesser: voffset, key, every fixed column, the record bytes and every lazy-getter "
+                   "pool (names, CIGAR, SEQ, QUAL, AUX, layout_ok), record by record")
+    return res, hc
+
+
 def free_port():
     import socket
     with socket.socket() as so:
@@ -264,13 +320,17 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity-splits", type=int, default=32)
+    ap.add_argument("--no-whole-check", action="store_true",
+                    help="skip the check of every record of the timed launch against the oracle")
     ap.add_argument("--sort-size", type=float, default=2e9,
                     help="N > 1: compressed bytes per GPU of the unsorted file of the Sort leg (config #5 "
                          "shape; 12.5e9 = config #5's per-GPU share at 8 GPUs)")
     ap.add_argument("--sort-steps", type=int, default=2)
     ap.add_argument("--no-sort", action="store_true", help="N > 1: skip the Sort leg")
-    ap.add_argument("--sort-timeout", type=float, default=600.0,
-                    help="N > 1: seconds before the Sort leg's watchdog ends the ranks (the line is printed)")
+    ap.add_argument("--deadline", type=float, default=420.0,
+                    help="N > 1: seconds from process start by which the Sort leg must end; its watchdog "
+                         "fires then (rank 0 prints the line with the leg's error, every rank exits 3), so "
+                         "a hung exchange never outlives the driver's limit with the headline unprinted")
     ap.add_argument("--config4", action="store_true",
                     help="BASELINE config #4 instead of the headline: ONE --c4-total file sharded over the N "
                          "GPUs (strong scaling), each rank's share resident, decoded in windows (tools/config4.py)")
@@ -392,21 +452,44 @@ def main():
         raise RuntimeError("decoded %d records (%d in boundary blocks read twice), generator wrote %d"
                            % (rec_all, ovl_all, gen_all))
     parity = None
-    if rank == 0 and args.parity_splits > 0:
+    whole_res = None
+    if not args.no_whole_check:
+        # every record of the timed launch against the oracle, on every rank (its own shard); at
+        # most WHOLE_CHECK_GROUP ranks hold their host copy (~2.3 x U) at once
+        for turn in range(0, world, WHOLE_CHECK_GROUP):
+            if turn <= rank < turn + WHOLE_CHECK_GROUP:
+                whole_res, hc = whole_shard_check(ctx, cols, buf, own_len, off, threads)
+                if rank == 0 and args.parity_splits > 0 and hc is not None:
+                    try:
+                        parity = parity_at_size(ctx, buf, dcomp[:len(buf)], args.parity_splits,
+                                                args.seed + 17, threads, whole=host_views(hc))
+                    except Exception as e:  # reported, never hidden
+                        parity = {"error": str(e)}
+                if hc is not None:
+                    ctx.L.hbam_free_host_columns(C.byref(hc))
+            if dist:
+                dist.barrier()
+        if dist:
+            # every rank's verdict to rank 0
+            mine = json.dumps(whole_res)
+            got = [None] * world
+            dist.all_gather_object(got, mine)
+            whole_res = [json.loads(x) for x in got]
+        else:
+            whole_res = [whole_res]
+    elif rank == 0 and args.parity_splits > 0:
         try:
-            # host copy of the timed decode's own output (before any other decode reuses the
-            # context's device buffers)
             hc = _lib.Columns()
-            rc = ctx.L.hbam_columns_to_host(ctx.h, C.byref(cols), C.byref(hc))
-            if rc:
+            if ctx.L.hbam_columns_to_host(ctx.h, C.byref(cols), C.byref(hc)):
                 raise RuntimeError("hbam_columns_to_host: %s" % ctx.last_error())
-            whole = _lib.host_columns_to_numpy(hc)
-            ctx.L.hbam_free_host_columns(C.byref(hc))
             parity = parity_at_size(ctx, buf, dcomp[:len(buf)], args.parity_splits, args.seed + 17,
-                                    threads, whole=whole)
-            del whole
+                                    threads, whole=host_views(hc))
+            ctx.L.hbam_free_host_columns(C.byref(hc))
         except Exception as e:  # reported, never hidden
             parity = {"error": str(e)}
+    if rank == 0 and whole_res is not None:
+        parity = parity if parity is not None else {}
+        parity["whole_launch"] = whole_res
     result = headline(args, world, elapsed, stages, huff_ms, ubytes, n_rec, own_len, file_len,
                       ub_all, rec_all, parity) if rank == 0 else None
     del cols
@@ -428,26 +511,44 @@ def main():
         dist.destroy_process_group()
 
 
+T_START = time.time()
+WATCHDOG_EXIT = 3
+SORT_LEG_MIN_S = 30.0  # a leg given less than this is skipped, not started
+
+
+def sort_leg_budget(deadline, elapsed):
+    """seconds the Sort leg may run: what is left of the whole-run deadline, or 0 (skip the leg)
+    when less than SORT_LEG_MIN_S is left"""
+    left = deadline - elapsed
+    return left if left >= SORT_LEG_MIN_S else 0.0
+
+
 def guarded_sort_leg(ctx, dist, rank, world, args, threads, dev, cdev, result):
     """The Sort leg under a watchdog.  Its exchange runs through libhbam's own RCCL communicator,
     which has no timeout of its own: if a rank fails, the others would wait in a collective for
-    ever.  An exception is reported in the line (never hidden); a leg that has not finished after
-    --sort-timeout seconds ends every rank's process (rank 0 first prints the headline line with
-    the Sort leg's error), so the headline measurement is never lost to the leg."""
+    ever.  An exception is reported in the line (never hidden); a leg still running at --deadline
+    seconds after process start ends every rank's process with status WATCHDOG_EXIT (rank 0 first
+    prints the headline line with the Sort leg's error), so the headline measurement is never lost
+    to the leg and the failure is still visible to the launcher."""
     import threading
     import sort_leg as sl
     done = threading.Event()
+    budget = sort_leg_budget(args.deadline, time.time() - T_START)
+    if budget <= 0:
+        return {"error": "skipped: %.0f s of the %.0f s deadline already used before the leg"
+                         % (time.time() - T_START, args.deadline)}
 
     def fire():
         if done.is_set():
             return
         if rank == 0 and result is not None:
-            result["sort"] = {"error": "timeout after %.0f s" % args.sort_timeout}
+            result["sort"] = {"error": "timeout: the leg did not end within the %.0f s deadline "
+                                       "(%.0f s for the leg)" % (args.deadline, budget)}
             print(json.dumps(result), flush=True)
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
-    tm = threading.Timer(args.sort_timeout, fire)
+        os._exit(WATCHDOG_EXIT)  # a hung or failed multi-GPU leg is a failure, not a pass
+    tm = threading.Timer(budget, fire)
     tm.daemon = True
     tm.start()
     try:

@@ -719,7 +719,65 @@ int stage_comp(hbam_ctx* c, const uint8_t* comp, int on_device, uint64_t len, co
   return HBAM_OK;
 }
 
-// host-side BAM header parse over inflated bytes (SAMHeaderReader / [htsjdk] BAMFileReader)
+// the @SQ lines of a SAM text header: SN value and LN, in order ([htsjdk] SAMTextHeaderCodec
+// parseSQLine under the reader's STRICT stringency: an @SQ line without SN or LN, or an LN that is
+// not an int, raises).  Returns false on such a line.
+struct SqEntry {
+  const uint8_t* name;
+  uint32_t name_len;
+  int32_t len;
+};
+bool text_sq_lines(const uint8_t* t, uint64_t n, std::vector<SqEntry>* out) {
+  out->clear();
+  for (uint64_t a = 0; a < n;) {
+    uint64_t e = a;
+    while (e < n && t[e] != '\n') ++e;
+    uint64_t z = e;
+    if (z > a && t[z - 1] == '\r') --z;  // "\r\n" ends a line too
+    if (z - a >= 3 && t[a] == '@' && t[a + 1] == 'S' && t[a + 2] == 'Q' && (z - a == 3 || t[a + 3] == '\t')) {
+      const uint8_t* sn = nullptr;
+      uint32_t sn_len = 0;
+      bool has_sn = false, has_ln = false;
+      int64_t ln = 0;
+      for (uint64_t f = a + 3; f < z;) {  // f at a '\t'
+        uint64_t g = f + 1;
+        while (g < z && t[g] != '\t') ++g;
+        const uint8_t* v = t + f + 1;
+        const uint64_t vl = g - f - 1;
+        if (vl >= 3 && v[2] == ':' && v[0] == 'S' && v[1] == 'N' && !has_sn) {
+          sn = v + 3;
+          sn_len = (uint32_t)(vl - 3);
+          has_sn = true;
+        } else if (vl >= 3 && v[2] == ':' && v[0] == 'L' && v[1] == 'N' && !has_ln) {
+          // Integer.parseInt: optional sign, then 1..10 digits within the int range
+          uint64_t k = 3;
+          bool neg = false;
+          if (k < vl && (v[k] == '-' || v[k] == '+')) neg = v[k++] == '-';
+          if (k == vl) return false;
+          for (; k < vl; ++k) {
+            if (v[k] < '0' || v[k] > '9') return false;
+            ln = ln * 10 + (v[k] - '0');
+            if (ln > 2147483648LL) return false;
+          }
+          if (neg) ln = -ln;
+          if (ln > 2147483647LL) return false;
+          has_ln = true;
+        }
+        f = g;
+      }
+      if (!has_sn || !has_ln) return false;
+      out->push_back({sn, sn_len, (int32_t)ln});
+    }
+    a = e + 1;
+  }
+  return true;
+}
+
+// host-side BAM header parse over inflated bytes (SAMHeaderReader.readSAMHeaderFrom,
+// SAMHeaderReader.java:53-72 -> [htsjdk] BAMFileReader.readHeader / readSequenceRecord): when the
+// text holds @SQ lines, the binary dictionary must match it entry by entry — the count, each
+// name (the binary name cut at its first whitespace, SAMSequenceUtil.truncateSequenceName) and
+// each length — and every binary entry needs a name (l_name > 1); all SAMFormatException
 int parse_header_bytes(const uint8_t* u, uint64_t n, hbam_header* h, bool* need_more) {
   *need_more = false;
   auto need = [&](uint64_t k) { return k > n; };
@@ -729,21 +787,27 @@ int parse_header_bytes(const uint8_t* u, uint64_t n, hbam_header* h, bool* need_
   if (l_text < 0) return HBAM_EFORMAT;
   uint64_t p = 8 + (uint64_t)l_text;
   if (need(p + 4)) { *need_more = true; return HBAM_OK; }
-  int32_t sq = 0;
-  for (int32_t i = 0; i + 3 < l_text; ++i)
-    if ((i == 0 || u[8 + i - 1] == '\n') && u[8 + i] == '@' && u[8 + i + 1] == 'S' && u[8 + i + 2] == 'Q')
-      ++sq;
+  std::vector<SqEntry> sq;
+  if (!text_sq_lines(u + 8, (uint64_t)l_text, &sq)) return HBAM_EFORMAT;
   const int32_t n_ref = rd32(u + p);
   if (n_ref < 0) return HBAM_EFORMAT;
+  if (!sq.empty() && sq.size() != (size_t)n_ref) return HBAM_EFORMAT;
   p += 4;
   for (int32_t i = 0; i < n_ref; ++i) {
     if (need(p + 4)) { *need_more = true; return HBAM_OK; }
     const int32_t ln = rd32(u + p);
-    if (ln <= 0) return HBAM_EFORMAT;
+    if (ln <= 1) return HBAM_EFORMAT;  // "missing sequence name"
+    if (need(p + 4 + (uint64_t)ln + 4)) { *need_more = true; return HBAM_OK; }
+    if (!sq.empty()) {
+      const uint8_t* nm = u + p + 4;
+      uint32_t k = 0;
+      while (k < (uint32_t)(ln - 1) && !(nm[k] == ' ' || (nm[k] >= 9 && nm[k] <= 13))) ++k;
+      const SqEntry& t = sq[(size_t)i];
+      if (t.name_len != k || memcmp(t.name, nm, k) != 0) return HBAM_EFORMAT;  // different names
+      if (t.len != rd32(u + p + 4 + (uint64_t)ln)) return HBAM_EFORMAT;        // different lengths
+    }
     p += 4 + (uint64_t)ln + 4;
-    if (need(p)) { *need_more = true; return HBAM_OK; }
   }
-  if (sq > 0 && sq != n_ref) return HBAM_EFORMAT;
   h->l_text = l_text;
   h->n_ref = n_ref;
   h->header_ulen = p;
@@ -1284,6 +1348,8 @@ struct hbam_split_stream {
   bool done = false;
   uint64_t h2d_bytes = 0, windows = 0;
   double h2d_ms = 0;
+  uint8_t* rec_host = nullptr;  // hbam_split_records_to_host: pinned, grow-only
+  size_t rec_host_cap = 0;
 };
 
 namespace {
@@ -1548,6 +1614,7 @@ extern "C" void hbam_split_close(hbam_split_stream* s) {
     if (s->e1[k]) (void)hipEventDestroy(s->e1[k]);
   }
   if (s->cs) (void)hipStreamDestroy(s->cs);
+  if (s->rec_host) (void)hipHostFree(s->rec_host);
   delete s;
 }
 
@@ -1642,17 +1709,20 @@ extern "C" void hbam_free_host_columns(hbam_columns* h) {
 }
 
 namespace {
-__global__ void k_rebase_off(const uint64_t* __restrict__ in, uint64_t n, uint64_t lo, uint64_t* __restrict__ out) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    out[i] = in[i] - lo;
+// rec_off rebased to the copied byte range; a record that does not end where the next one starts
+// (columns that are not a decoded split's contiguous, ascending records) raises *bad
+__global__ void k_rebase_off(const uint64_t* __restrict__ in, const int32_t* __restrict__ bs, uint64_t n,
+                             uint64_t lo, uint64_t* __restrict__ out, uint32_t* __restrict__ bad) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = in[i];
+    out[i] = r - lo;
+    if (i + 1 < n && in[i + 1] != r + 4u + (uint64_t)(uint32_t)bs[i]) *bad = 1u;
+  }
 }
-}  // namespace
 
-// Records-only host copy for the drop-in reader (BAMRecordReader.nextKeyValue, :172-188, needs a
-// record's bytes, its key and its file pointer): 28 B of columns per record + the records' bytes,
-// into the context's pinned staging (one D2H pass at the DMA rate, no malloc per window).
-extern "C" int hbam_records_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_columns* h) {
-  if (!c || !dv || !h) return HBAM_EINVAL;
+// Records-only host copy (hbam_records_to_host / hbam_split_records_to_host) into the pinned
+// staging *stage (grow-only, *cap bytes)
+int records_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_columns* h, uint8_t** stage, size_t* cap) {
   HIPCHK(c, hipSetDevice(c->device));
   memset(h, 0, sizeof *h);
   const uint64_t n = dv->n_records;
@@ -1672,24 +1742,28 @@ extern "C" int hbam_records_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_co
     return set_err(c, HBAM_EINVAL, "hbam_records_to_host: record bytes outside ubuf");
   const size_t cols = 8 * n * 3 + ((4 * n + 7) & ~(size_t)7);
   const size_t need = cols + (hi - lo) + 64;
-  if (c->rec_host_cap < need) {
-    if (c->rec_host) (void)hipHostFree(c->rec_host);
-    c->rec_host = nullptr;
-    c->rec_host_cap = 0;
+  if (*cap < need) {
+    if (*stage) (void)hipHostFree(*stage);
+    *stage = nullptr;
+    *cap = 0;
     const size_t want = std::max(need, need + need / 4);
-    if (hipHostMalloc((void**)&c->rec_host, want, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void**)stage, want, hipHostMallocDefault) != hipSuccess) {
       (void)hipGetLastError();
-      c->rec_host = nullptr;
+      *stage = nullptr;
       return set_err(c, HBAM_ENOMEM, "hbam_records_to_host: hipHostMalloc(%zu) failed", want);
     }
-    c->rec_host_cap = want;
+    *cap = want;
   }
   uint64_t* roff;
+  uint32_t* bad;
   int rc;
-  if ((rc = ensure(c, B_RH_RECOFF, n, &roff))) return rc;
-  k_rebase_off<<<(uint32_t)std::min<uint64_t>(grid_for(n, 256), 16384), 256, 0, c->stream>>>(dv->rec_off, n, lo, roff);
+  if ((rc = ensure(c, B_RH_RECOFF, n + 1, &roff))) return rc;
+  bad = (uint32_t*)(roff + n);
+  HIPCHK(c, hipMemsetAsync(bad, 0, 4, c->stream));
+  k_rebase_off<<<(uint32_t)std::min<uint64_t>(grid_for(n, 256), 16384), 256, 0, c->stream>>>(dv->rec_off, dv->block_size,
+                                                                                             n, lo, roff, bad);
   HIPCHK(c, hipGetLastError());
-  uint8_t* p = c->rec_host;
+  uint8_t* p = *stage;
   h->voffset = (uint64_t*)p;
   h->key = (int64_t*)(p + 8 * n);
   h->rec_off = (uint64_t*)(p + 16 * n);
@@ -1701,12 +1775,34 @@ extern "C" int hbam_records_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_co
   HIPCHK(c, hipMemcpyAsync(h->rec_off, roff, 8 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(h->block_size, dv->block_size, 4 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(h->ubuf, dv->ubuf + lo, hi - lo, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->pinned_small + 3, bad, 4, hipMemcpyDeviceToHost, c->stream));
   const hipError_t e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     memset(h, 0, sizeof *h);
     return set_err(c, HBAM_EDEVICE, "hbam_records_to_host: %s", hipGetErrorString(e));
   }
+  if ((uint32_t)c->pinned_small[3]) {
+    memset(h, 0, sizeof *h);
+    return set_err(c, HBAM_EINVAL, "hbam_records_to_host: records are not contiguous in ubuf (not a decoded split's "
+                                   "columns)");
+  }
   return HBAM_OK;
+}
+}  // namespace
+
+// Records-only host copy for the drop-in reader (BAMRecordReader.nextKeyValue, :172-188, needs a
+// record's bytes, its key and its file pointer): 28 B of columns per record + the records' bytes,
+// into the context's pinned staging (one D2H pass at the DMA rate, no malloc per window).
+extern "C" int hbam_records_to_host(hbam_ctx* c, const hbam_columns* dv, hbam_columns* h) {
+  if (!c || !dv || !h) return HBAM_EINVAL;
+  return records_to_host(c, dv, h, &c->rec_host, &c->rec_host_cap);
+}
+
+// The same into the split stream's own staging: each reader of a context keeps its window's host
+// copy while other streams of the context read theirs
+extern "C" int hbam_split_records_to_host(hbam_split_stream* s, const hbam_columns* dv, hbam_columns* h) {
+  if (!s || !dv || !h) return HBAM_EINVAL;
+  return records_to_host(s->c, dv, h, &s->rec_host, &s->rec_host_cap);
 }
 
 extern "C" void hbam_release_columns(hbam_ctx* c, hbam_columns* dv) {

@@ -19,6 +19,11 @@
 
 #include <rccl/rccl.h>
 
+// largest single point-to-point transfer of the Sort exchange (bytes)
+#ifndef HBAM_XCHG_CHUNK
+#define HBAM_XCHG_CHUNK (1ull << 30)
+#endif
+
 namespace {
 
 struct RcclApi {
@@ -261,6 +266,25 @@ extern "C" int hbam_sort_exchange(hbam_ctx* c, hbam_comm* m, const hbam_sorted_r
       (rc = ensure(c, B_X_BS, nr + 1, &rs)) || (rc = ensure(c, B_X_PAY, nb + 1, &rp)))
     return rc;
   HIPCHK(c, hipEventRecord(c->ev[12], c->stream));
+  // every transfer goes out in pieces of at most HBAM_XCHG_CHUNK bytes: a peer's payload at config
+  // #5 is several GB, and no single point-to-point call above 2 GiB has been exercised; both sides
+  // cut a (sender, receiver) pair's bytes at the same offsets, and RCCL matches the pieces in order
+  auto send = [&](const void* ptr, uint64_t bytes, int peer) -> ncclResult_t {
+    for (uint64_t o = 0; o < bytes; o += HBAM_XCHG_CHUNK) {
+      const ncclResult_t r = R.Send((const uint8_t*)ptr + o, std::min<uint64_t>(HBAM_XCHG_CHUNK, bytes - o),
+                                    ncclUint8, peer, m->comm, c->stream);
+      if (r != ncclSuccess) return r;
+    }
+    return ncclSuccess;
+  };
+  auto recv = [&](void* ptr, uint64_t bytes, int peer) -> ncclResult_t {
+    for (uint64_t o = 0; o < bytes; o += HBAM_XCHG_CHUNK) {
+      const ncclResult_t r = R.Recv((uint8_t*)ptr + o, std::min<uint64_t>(HBAM_XCHG_CHUNK, bytes - o), ncclUint8,
+                                    peer, m->comm, c->stream);
+      if (r != ncclSuccess) return r;
+    }
+    return ncclSuccess;
+  };
   GroupGuard group;
   NCCLCHK(c, group.start());
   for (uint32_t p = 0; p < P; ++p) {
@@ -268,16 +292,16 @@ extern "C" int hbam_sort_exchange(hbam_ctx* c, hbam_comm* m, const hbam_sorted_r
     const uint64_t rr = roff[p + 1] - roff[p], rbb = rboff[p + 1] - rboff[p];
     const uint64_t r0 = m->rec_b[p], b0 = m->byte_b[p];
     if (sr) {
-      NCCLCHK(c, R.Send(run->key + r0, sr * 8, ncclUint8, (int)p, m->comm, c->stream));
-      NCCLCHK(c, R.Send(run->voffset + r0, sr * 8, ncclUint8, (int)p, m->comm, c->stream));
-      NCCLCHK(c, R.Send(run->block_size + r0, sr * 4, ncclUint8, (int)p, m->comm, c->stream));
-      NCCLCHK(c, R.Send(run->payload + b0, sb, ncclUint8, (int)p, m->comm, c->stream));
+      NCCLCHK(c, send(run->key + r0, sr * 8, (int)p));
+      NCCLCHK(c, send(run->voffset + r0, sr * 8, (int)p));
+      NCCLCHK(c, send(run->block_size + r0, sr * 4, (int)p));
+      NCCLCHK(c, send(run->payload + b0, sb, (int)p));
     }
     if (rr) {
-      NCCLCHK(c, R.Recv(rk + roff[p], rr * 8, ncclUint8, (int)p, m->comm, c->stream));
-      NCCLCHK(c, R.Recv(rv + roff[p], rr * 8, ncclUint8, (int)p, m->comm, c->stream));
-      NCCLCHK(c, R.Recv(rs + roff[p], rr * 4, ncclUint8, (int)p, m->comm, c->stream));
-      NCCLCHK(c, R.Recv(rp + rboff[p], rbb, ncclUint8, (int)p, m->comm, c->stream));
+      NCCLCHK(c, recv(rk + roff[p], rr * 8, (int)p));
+      NCCLCHK(c, recv(rv + roff[p], rr * 8, (int)p));
+      NCCLCHK(c, recv(rs + roff[p], rr * 4, (int)p));
+      NCCLCHK(c, recv(rp + rboff[p], rbb, (int)p));
     }
   }
   NCCLCHK(c, group.end());

@@ -31,7 +31,7 @@ namespace hbam {
 #define HBAM_RS_W 512
 #endif
 #ifndef HBAM_RS_S
-#define HBAM_RS_S 1024  // A/B at 2 GB (window 1 KiB): 2048 -> 16.8 ms, 1024 -> 11.7 ms
+#define HBAM_RS_S 1024  // A/B at 2 GB (window 1 KiB): 2048 -> 16.8 ms, 1024 -> 11.7 ms; k_resolve_units needs 1024
 #endif
 constexpr uint32_t RS_S = HBAM_RS_S;                  // stretch (output bytes): 1024 or 2048
 constexpr uint32_t RS_C = RS_S / 1024;                // 16-byte columns per lane per stretch

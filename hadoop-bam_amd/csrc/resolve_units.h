@@ -28,6 +28,9 @@
 // match except the last: 342 matches starting in a stretch, plus the 17 extra units of a final
 // 258-byte match, at most
 constexpr uint32_t RU_CAP = 360;
+// RU_CAP and the 11-bit destination field of a unit record (rel < RS_S + 258 <= 2047) are sized for
+// 1 KiB stretches: a 2 KiB stretch would overrun both silently
+static_assert(RS_S == 1024, "k_resolve_units: unit capacity and record packing assume 1 KiB stretches");
 
 // unit record: bits 0-10 destination - s0 (< RS_S + 258), 11-14 bytes - 1, 15-29 distance - 1,
 // bit 30: periodic head unit (distance < 8 < bytes)

@@ -60,7 +60,7 @@ EXPORTS = [
     "hbam_host_register", "hbam_host_unregister", "hbam_bcf_parse_header", "hbam_guess_bcf_window_len",
     "hbam_guess_bcf_windows", "hbam_bcf_decode_split", "hbam_comm_unique_id", "hbam_comm_init",
     "hbam_comm_destroy", "hbam_comm_split_points", "hbam_sort_exchange", "hbam_split_open_reader",
-    "hbam_split_read_bytes", "hbam_rewrite_groups", "hbam_records_to_host",
+    "hbam_split_read_bytes", "hbam_rewrite_groups", "hbam_records_to_host", "hbam_split_records_to_host",
 ]
 
 # hbam_read_fn: int64_t read(void* user, uint64_t offset, uint64_t len, uint8_t* dst)
@@ -191,6 +191,7 @@ def load(path=None):
         "hbam_columns_to_host": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(Columns)]),
         "hbam_free_host_columns": (None, [C.POINTER(Columns)]),
         "hbam_records_to_host": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(Columns)]),
+        "hbam_split_records_to_host": (C.c_int, [vp, C.POINTER(Columns), C.POINTER(Columns)]),
         "hbam_release_columns": (None, [vp, C.POINTER(Columns)]),
         "hbam_guess_bam_record_start": (C.c_int64, [vp, vp, C.c_int, C.c_uint64, C.c_int64,
                                                     C.c_int64, C.c_int32, _i32p]),
@@ -478,7 +479,7 @@ class Context:
                     yield d
                     continue
                 if host == "records":
-                    yield self.records_to_host(d)
+                    yield self.records_to_host(d, stream=s)
                     continue
                 h = Columns()
                 rc = self.L.hbam_columns_to_host(self.h, C.byref(d), C.byref(h))
@@ -492,12 +493,17 @@ class Context:
             self.L.hbam_split_close(s)
             del keep
 
-    def records_to_host(self, d):
+    def records_to_host(self, d, stream=None):
         """hbam_records_to_host: what the drop-in reader hands out (key, voffset, rec_off, block_size
         and the records' bytes), as numpy VIEWS of the context's pinned staging — valid until the
-        next call on this context.  d2h_bytes = what crossed PCIe."""
+        next call on this context; with `stream` (a split stream handle) hbam_split_records_to_host,
+        views of that stream's own staging, valid until its next window or close whatever other
+        readers of the context do.  d2h_bytes = what crossed PCIe."""
         h = Columns()
-        rc = self.L.hbam_records_to_host(self.h, C.byref(d), C.byref(h))
+        if stream is not None:
+            rc = self.L.hbam_split_records_to_host(stream, C.byref(d), C.byref(h))
+        else:
+            rc = self.L.hbam_records_to_host(self.h, C.byref(d), C.byref(h))
         if rc:
             raise RuntimeError("hbam_records_to_host failed (%d): %s" % (rc, self.last_error()))
         n = int(h.n_records)

@@ -194,8 +194,12 @@ int hbam_columns_to_host(hbam_ctx* ctx, const hbam_columns* dev, hbam_columns* h
  * voffset, block_size, rec_off (relative to host->ubuf) and ubuf = exactly the records' bytes
  * (each record's block_size field + record); every other pointer is NULL.  The arrays live in
  * pinned host memory owned by the context, valid until the next hbam_records_to_host or
- * hbam_destroy on it (never pass them to hbam_free_host_columns).  Copies 28 B per record plus
- * the record bytes (columns_to_host copies every pool too: about twice as much). */
+ * hbam_destroy on it (never pass them to hbam_free_host_columns): one consumer per context — a
+ * reader among several on one context takes hbam_split_records_to_host instead.  Copies 28 B per
+ * record plus the record bytes (columns_to_host copies every pool too: about twice as much).
+ * Precondition: `dev` holds a decoded split's columns (hbam_decode_split, hbam_split_next,
+ * hbam_rewrite_groups), whose records lie back to back in ubuf in index order; columns whose
+ * records are permuted or not contiguous return HBAM_EINVAL. */
 int hbam_records_to_host(hbam_ctx* ctx, const hbam_columns* dev, hbam_columns* host);
 /* Streamed split read: BAMRecordReader over FileVirtualSplit
  * [v_start, v_end) of a file the caller holds in host memory (e.g. mmap; only the split's
@@ -227,6 +231,10 @@ int hbam_split_next(hbam_split_stream* s, hbam_columns* out);
 int hbam_split_stats(const hbam_split_stream* s, uint64_t* h2d_bytes, double* h2d_ms, uint64_t* windows);
 uint64_t hbam_split_read_bytes(const hbam_split_stream* s);
 void hbam_split_close(hbam_split_stream* s);
+/* hbam_records_to_host into the split stream's own pinned staging: valid until the next call on
+ * this stream or hbam_split_close, whatever other streams of the same context do (the drop-in
+ * readers: several BAMRecordReaders may share one context). */
+int hbam_split_records_to_host(hbam_split_stream* s, const hbam_columns* dev, hbam_columns* host);
 void hbam_free_host_columns(hbam_columns* host);
 void hbam_release_columns(hbam_ctx* ctx, hbam_columns* dev);
 

@@ -41,6 +41,9 @@ public final class Hbam implements AutoCloseable {
   // the drop-in reader's copy: key, voffset, rec_off, block_size + record bytes (context-owned, pinned)
   static final MethodHandle RECORDS_TO_HOST = fn("hbam_records_to_host",
       FunctionDescriptor.of(I, A, A, A));
+  // the same into the split stream's own pinned staging (readers sharing a context stay apart)
+  static final MethodHandle SPLIT_RECORDS_TO_HOST = fn("hbam_split_records_to_host",
+      FunctionDescriptor.of(I, A, A, A));
   static final MethodHandle SPLIT_OPEN = fn("hbam_split_open",
       FunctionDescriptor.of(A, A, A, J, J, J, I, J));
   static final MethodHandle SPLIT_NEXT = fn("hbam_split_next", FunctionDescriptor.of(I, A, A));

@@ -120,11 +120,11 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     return cols.get(ValueLayout.ADDRESS, Hbam.offsetOf(f)).reinterpret(Math.max(bytes, 1));
   }
 
-  /** The next window's records (hbam_split_next + hbam_records_to_host); false at the end. */
+  /** The next window's records (hbam_split_next + hbam_split_records_to_host); false at the end. */
   private boolean nextWindow() {
     long bad = -1;  // first record hbam_merge_remap refuses (HipSortRecordReader only)
     try {
-      hostLive = false;  // the previous window's host copy is the context's staging: reused below
+      hostLive = false;  // the previous window's host copy is the stream's staging: reused below
       final int rc = (int) Hbam.SPLIT_NEXT.invokeExact(stream, dev);
       if (rc < 0) {
         if (source.failure() != null) throw new RuntimeIOException(source.failure());
@@ -155,9 +155,9 @@ public class HipBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
         }
       }
       // only what nextKeyValue reads: key, voffset, rec_off, block_size and the record bytes, into
-      // the context's pinned staging (hbam_records_to_host; no pool crosses PCIe)
-      final int rc2 = (int) Hbam.RECORDS_TO_HOST.invokeExact(hbam.context(), dev, host);
-      if (rc2 != Hbam.OK) throw new RuntimeIOException("hbam_records_to_host: " + hbam.lastError());
+      // the split stream's pinned staging (hbam_split_records_to_host; no pool crosses PCIe)
+      final int rc2 = (int) Hbam.SPLIT_RECORDS_TO_HOST.invokeExact(stream, dev, host);
+      if (rc2 != Hbam.OK) throw new RuntimeIOException("hbam_split_records_to_host: " + hbam.lastError());
       hostLive = true;
     } catch (RuntimeException e) {
       throw e;

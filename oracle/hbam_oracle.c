@@ -444,9 +444,71 @@ int64_t or_scan_blocks(const uint8_t* f, uint64_t len, uint64_t* coff, uint32_t*
 }
 
 /* ------------------------------------------------------------------------------ */
+/* [htsjdk] SAMTextHeaderCodec.parseSQLine under STRICT stringency (the reader's default): the @SQ
+ * lines of the text, in order, with their SN value and LN.  An @SQ line without SN or LN, or an LN
+ * Integer.parseInt rejects, raises (returns -1).  Returns the number of @SQ lines. */
+typedef struct sq_entry {
+  const uint8_t* name;
+  int32_t name_len;
+  int32_t len;
+} sq_entry;
+
+static int32_t text_sq(const uint8_t* t, int32_t n, sq_entry** out) {
+  int32_t cnt = 0, cap = 0;
+  *out = NULL;
+  for (int32_t a = 0; a < n;) {
+    int32_t e = a;
+    while (e < n && t[e] != '\n') ++e;
+    int32_t z = e;
+    if (z > a && t[z - 1] == '\r') --z; /* StringLineReader: "\r\n" ends a line */
+    if (z - a >= 3 && memcmp(t + a, "@SQ", 3) == 0 && (z - a == 3 || t[a + 3] == '\t')) {
+      sq_entry x = {NULL, 0, 0};
+      int has_sn = 0, has_ln = 0;
+      for (int32_t f = a + 3; f < z;) { /* tab-separated TAG:value fields */
+        int32_t g = f + 1;
+        while (g < z && t[g] != '\t') ++g;
+        const uint8_t* v = t + f + 1;
+        const int32_t vl = g - f - 1;
+        if (vl >= 3 && v[2] == ':' && v[0] == 'S' && v[1] == 'N' && !has_sn) {
+          x.name = v + 3;
+          x.name_len = vl - 3;
+          has_sn = 1;
+        } else if (vl >= 3 && v[2] == ':' && v[0] == 'L' && v[1] == 'N' && !has_ln) {
+          int32_t k = 3, neg = 0;
+          int64_t ln = 0;
+          if (k < vl && (v[k] == '-' || v[k] == '+')) neg = v[k++] == '-';
+          if (k == vl) { free(*out); *out = NULL; return -1; }
+          for (; k < vl; ++k) {
+            if (v[k] < '0' || v[k] > '9' || (ln = ln * 10 + (v[k] - '0')) > 2147483648LL) { free(*out); *out = NULL; return -1; }
+          }
+          if (neg) ln = -ln;
+          if (ln > 2147483647LL) { free(*out); *out = NULL; return -1; }
+          x.len = (int32_t)ln;
+          has_ln = 1;
+        }
+        f = g;
+      }
+      if (!has_sn || !has_ln) { free(*out); *out = NULL; return -1; }
+      if (cnt == cap) {
+        cap = cap ? 2 * cap : 64;
+        sq_entry* np = (sq_entry*)realloc(*out, (size_t)cap * sizeof *np);
+        if (!np) { free(*out); *out = NULL; return -1; }
+        *out = np;
+      }
+      (*out)[cnt++] = x;
+    }
+    a = e + 1;
+  }
+  return cnt;
+}
+
 /* SAMHeaderReader.readSAMHeaderFrom (util/SAMHeaderReader.java:53-72) for BAM:
- * [htsjdk] BAMFileReader.readHeader — magic, l_text, text, n_ref, {l_name,name,l_ref}.
- * Text @SQ count must equal n_ref when present (SAMFormatException otherwise). */
+ * [htsjdk] BAMFileReader.readHeader — magic, l_text, text, n_ref, {l_name,name,l_ref}.  When the
+ * text holds @SQ lines the binary dictionary must match them: the count (checked before any
+ * entry is read), then per entry the name (the binary one cut at its first whitespace,
+ * SAMSequenceUtil.truncateSequenceName) and the length; readSequenceRecord rejects l_name <= 1
+ * ("missing sequence name").  All SAMFormatException.  Restated from htsjdk 1.131's published
+ * source (absent here: parity unpinned). */
 int or_read_header(const uint8_t* f, uint64_t len, or_header* h) {
   ostream s = {f, (int64_t)len, 0};
   bcis* b = bcis_new(&s, 0);
@@ -454,6 +516,9 @@ int or_read_header(const uint8_t* f, uint64_t len, or_header* h) {
   int rc;
   uint8_t t[4];
   uint8_t* text = NULL;
+  uint8_t* name = NULL;
+  sq_entry* sq = NULL;
+  int32_t nsq = 0;
 #define HR(buf, n)                                   \
   do {                                               \
     rc = codec_read_bytes(b, (buf), (n));            \
@@ -467,30 +532,29 @@ int or_read_header(const uint8_t* f, uint64_t len, or_header* h) {
   text = (uint8_t*)malloc((size_t)h->l_text + 1);
   if (!text) { rc = OR_ENOMEM; goto out; }
   if (h->l_text) HR(text, h->l_text);
+  nsq = text_sq(text, h->l_text, &sq);
+  if (nsq < 0) { rc = OR_EFORMAT; goto out; }
   HR(t, 4);
   h->n_ref = rd_i32(t);
   if (h->n_ref < 0) { rc = OR_EFORMAT; goto out; }
+  if (nsq > 0 && nsq != h->n_ref) { rc = OR_EFORMAT; goto out; }
   uint64_t ulen = 12 + (uint64_t)h->l_text;
   for (int32_t i = 0; i < h->n_ref; ++i) {
     HR(t, 4);
     int32_t ln = rd_i32(t);
-    if (ln <= 0) { rc = OR_EFORMAT; goto out; }
-    uint8_t nb[256];
-    for (int32_t k = 0; k < ln;) {
-      int32_t c = ln - k < 256 ? ln - k : 256;
-      HR(nb, c);
-      k += c;
-    }
+    if (ln <= 1) { rc = OR_EFORMAT; goto out; }
+    free(name);
+    name = (uint8_t*)malloc((size_t)ln);
+    if (!name) { rc = OR_ENOMEM; goto out; }
+    HR(name, ln);
     HR(t, 4);
+    if (nsq > 0) {
+      int32_t k = 0;
+      while (k < ln - 1 && !(name[k] == ' ' || (name[k] >= 9 && name[k] <= 13))) ++k;
+      if (sq[i].name_len != k || memcmp(sq[i].name, name, (size_t)k) != 0) { rc = OR_EFORMAT; goto out; }
+      if (sq[i].len != rd_i32(t)) { rc = OR_EFORMAT; goto out; }
+    }
     ulen += 8 + (uint64_t)ln;
-  }
-  {
-    /* count @SQ lines in the text */
-    int32_t sq = 0;
-    for (int32_t i = 0; i + 3 < h->l_text; ++i)
-      if ((i == 0 || text[i - 1] == '\n') && text[i] == '@' && text[i + 1] == 'S' && text[i + 2] == 'Q')
-        ++sq;
-    if (sq > 0 && sq != h->n_ref) { rc = OR_EFORMAT; goto out; }
   }
   h->header_ulen = ulen;
   h->first_voffset = bcis_tell(b);
@@ -499,6 +563,8 @@ out:
 #undef HR
   if (rc == OR_EEOF || rc == OR_ERUNTIMEIO) rc = OR_EFORMAT;
   free(text);
+  free(name);
+  free(sq);
   bcis_free(b);
   return rc;
 }
@@ -858,8 +924,15 @@ int64_t or_probabilistic_splits(const uint8_t* f, uint64_t len, const uint64_t* 
   or_header h;
   int rc = or_read_header(f, len, &h);
   if (rc) return rc;
+  return or_probabilistic_splits_nref(f, len, beg, end, n, h.n_ref, v_start, v_end);
+}
+
+/* the same over a window of the file whose header was read elsewhere (n_ref given) */
+int64_t or_probabilistic_splits_nref(const uint8_t* f, uint64_t len, const uint64_t* beg,
+                                     const uint64_t* end, uint64_t n, int32_t n_ref,
+                                     uint64_t* v_start, uint64_t* v_end) {
   if (len < 4 || rd_i32(f) != BGZF_MAGIC) return OR_EFORMAT;
-  guesser* g = guesser_new(f, len, h.n_ref);
+  guesser* g = guesser_new(f, len, n_ref);
   if (!g) return OR_ENOMEM;
   int64_t out = 0;
   for (uint64_t i = 0; i < n; ++i) {
@@ -1098,6 +1171,93 @@ void or_cols_free(or_cols* c) {
   free(c->l_seq); free(c->next_ref_id); free(c->next_pos); free(c->tlen); free(c->var_off);
   free(c->var);
   memset(c, 0, sizeof *c);
+}
+
+/* ------------------------------------------------------------------------------ */
+/* Whole-output checker (test infrastructure: bench.py's at-size parity).            */
+enum {
+  CK_COUNT = 1, CK_VOFFSET, CK_KEY, CK_FIXED, CK_BYTES, CK_LAYOUT, CK_NAMES, CK_CIGARS, CK_SEQ,
+  CK_QUAL, CK_AUX
+};
+
+typedef struct check_ctx {
+  const or_dev_cols* d;
+  uint64_t next;  /* device index of the next oracle record */
+  or_check* out;
+} check_ctx;
+
+static const char SEQ_ALPHA[] = "=ACMGRSVTWYHKDBN";
+
+static int check_one(const or_dev_cols* d, uint64_t i, const or_record* r) {
+  if (i >= d->n) return CK_COUNT;
+  if (d->voffset[i] != r->voffset + d->voff_base) return CK_VOFFSET;
+  if (d->key[i] != r->key) return CK_KEY;
+  if (d->block_size[i] != r->block_size || d->ref_id[i] != r->ref_id || d->pos[i] != r->pos ||
+      d->l_read_name[i] != r->l_read_name || d->mapq[i] != r->mapq || d->bin[i] != r->bin ||
+      d->n_cigar[i] != r->n_cigar || d->flag[i] != r->flag || d->l_seq[i] != r->l_seq ||
+      d->next_ref_id[i] != r->next_ref_id || d->next_pos[i] != r->next_pos || d->tlen[i] != r->tlen)
+    return CK_FIXED;
+  /* the record's bytes as the device holds them (rec_off: its block_size field) */
+  const int64_t vlen = (int64_t)r->block_size - 32;
+  if (d->rec_off[i] + 4u + (uint64_t)r->block_size > d->ubuf_len) return CK_BYTES;
+  if (vlen > 0 && memcmp(d->ubuf + d->rec_off[i] + 36, r->var, (size_t)vlen) != 0) return CK_BYTES;
+  /* lazy getters' pools (oracle.pools restated per record) */
+  int64_t L = r->l_read_name, nc = r->n_cigar, ls = r->l_seq;
+  const int64_t fixed = L + 4 * nc + (ls + 1) / 2 + ls;
+  const int ok = ls >= 0 && fixed <= vlen;
+  if (d->layout_ok[i] != (uint8_t)ok) return CK_LAYOUT;
+  int64_t na = ok ? vlen - fixed : 0;
+  if (!ok) L = nc = ls = 0;
+  const uint8_t* v = r->var;
+  if ((int64_t)(d->name_off[i + 1] - d->name_off[i]) != L ||
+      (L && memcmp(d->names + d->name_off[i], v, (size_t)L) != 0))
+    return CK_NAMES;
+  if ((int64_t)(d->cigar_off[i + 1] - d->cigar_off[i]) != nc ||
+      (nc && memcmp(d->cigars + d->cigar_off[i], v + L, (size_t)(4 * nc)) != 0))
+    return CK_CIGARS;
+  if ((int64_t)(d->seq_off[i + 1] - d->seq_off[i]) != ls) return CK_SEQ;
+  const uint8_t* sp = v + L + 4 * nc;
+  const uint8_t* ds = d->seq + d->seq_off[i];
+  for (int64_t k = 0; k < ls; ++k) {
+    const uint8_t nib = (k & 1) ? (sp[k >> 1] & 15) : (sp[k >> 1] >> 4);
+    if (ds[k] != (uint8_t)SEQ_ALPHA[nib]) return CK_SEQ;
+  }
+  const uint8_t* qp = sp + (ls + 1) / 2;
+  if (ls && memcmp(d->qual + d->seq_off[i], qp, (size_t)ls) != 0) return CK_QUAL;
+  if ((int64_t)(d->aux_off[i + 1] - d->aux_off[i]) != na ||
+      (na && memcmp(d->aux + d->aux_off[i], qp + ls, (size_t)na) != 0))
+    return CK_AUX;
+  return 0;
+}
+
+static int check_cb(void* user, const or_record* r) {
+  check_ctx* x = (check_ctx*)user;
+  const uint64_t i = x->next++;
+  const int f = check_one(x->d, i, r);
+  ++x->out->n_checked;
+  if (f) {
+    if (x->out->first_bad < 0) {
+      x->out->first_bad = (int64_t)i;
+      x->out->bad_field = f;
+    }
+    ++x->out->mismatches;
+    if (f == CK_COUNT) return 1;  /* past the device's records: nothing more to compare */
+  }
+  return 0;
+}
+
+int or_check_split(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                   const or_dev_cols* dev, uint64_t first, or_check* out) {
+  memset(out, 0, sizeof *out);
+  out->first_bad = -1;
+  check_ctx x = {dev, first, out};
+  or_read_result res;
+  if (n_ref < 0)
+    or_read_split(f, len, v_start, v_end, 0, check_cb, &x, &res);
+  else
+    read_split_body(f, len, v_start, v_end, 0, n_ref, check_cb, &x, &res);
+  out->status = res.status;
+  return res.status;
 }
 
 /* BCF read path: shares the stream model above */

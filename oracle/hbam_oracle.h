@@ -154,6 +154,48 @@ int or_read_split_cols_nref(const uint8_t* f, uint64_t len, uint64_t v_start, ui
                             int check_crc, int keep_var, int32_t n_ref, or_cols* out);
 void or_cols_free(or_cols* c);
 
+/* addProbabilisticSplits over a window of the file (a byte-range shard without the header):
+ * the same as or_probabilistic_splits with the dictionary size given. */
+int64_t or_probabilistic_splits_nref(const uint8_t* f, uint64_t len, const uint64_t* beg,
+                                     const uint64_t* end, uint64_t n, int32_t n_ref,
+                                     uint64_t* v_start, uint64_t* v_end);
+
+/* ---- whole-output checker (bench.py's at-size parity; test infrastructure) ----------------
+ * A decode's host copy (the device path's columns, pools and record bytes, record i at index i),
+ * compared record by record with the oracle's read of one FileVirtualSplit: every fixed column,
+ * the key, the voffset (+ voff_base), the record's variable bytes and every lazy-getter pool
+ * (names incl. NUL, CIGAR u32s, SEQ as "=ACMGRSVTWYHKDBN" characters, QUAL, AUX, layout_ok).
+ * The split's records are expected at device indices [first, first + n). */
+typedef struct or_dev_cols {
+  uint64_t n;
+  uint64_t voff_base;
+  const uint64_t* voffset;
+  const int64_t* key;
+  const uint64_t* rec_off;
+  const uint8_t* ubuf;
+  uint64_t ubuf_len;
+  const int32_t *block_size, *ref_id, *pos;
+  const uint8_t *l_read_name, *mapq;
+  const uint16_t *bin, *n_cigar, *flag;
+  const int32_t *l_seq, *next_ref_id, *next_pos, *tlen;
+  const uint8_t* layout_ok;
+  const uint64_t *name_off, *cigar_off, *seq_off, *aux_off; /* n+1; cigar_off counts u32s */
+  const uint8_t* names;
+  const uint32_t* cigars;
+  const uint8_t *seq, *qual, *aux;
+} or_dev_cols;
+
+typedef struct or_check {
+  uint64_t n_checked;    /* oracle records compared */
+  uint64_t mismatches;   /* records that differ in any field */
+  int64_t first_bad;     /* device index of the first differing record, -1 if none */
+  int32_t bad_field;     /* which field differed first (see hbam_oracle.c: CK_*) */
+  int32_t status;        /* the oracle read's status (0, or the exception it raised) */
+} or_check;
+
+int or_check_split(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                   const or_dev_cols* dev, uint64_t first, or_check* out);
+
 
 /* ---- read-name / CIGAR keyed consumers (hbam_oracle_f4.c) ----------------
  * Records are SAMRecordWritable payloads (block_size + record) at pay + off[i]. */

@@ -62,6 +62,12 @@ def lib():
         L.or_read_split_cols.restype = C.c_int
         L.or_read_split_cols.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_int,
                                          C.POINTER(OrCols)]
+        L.or_probabilistic_splits_nref.restype = C.c_int64
+        L.or_probabilistic_splits_nref.argtypes = [u8p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
+                                                   C.c_int32, C.c_void_p, C.c_void_p]
+        L.or_check_split.restype = C.c_int
+        L.or_check_split.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int32, C.c_void_p,
+                                     C.c_uint64, C.c_void_p]
         L.or_cols_free.restype = None
         L.or_cols_free.argtypes = [C.POINTER(OrCols)]
         vp = C.c_void_p
@@ -219,6 +225,89 @@ def probabilistic_splits(data, beg, end):
     return vs[:n], ve[:n]
 
 
+def probabilistic_splits_nref(data, beg, end, n_ref):
+    """addProbabilisticSplits over a window of the file (no header in `data`)"""
+    a, p = _buf(data)
+    beg = np.ascontiguousarray(beg, np.uint64)
+    end = np.ascontiguousarray(end, np.uint64)
+    vs = np.zeros(len(beg), np.uint64)
+    ve = np.zeros(len(beg), np.uint64)
+    n = lib().or_probabilistic_splits_nref(p, len(a), beg.ctypes.data, end.ctypes.data, len(beg), n_ref,
+                                           vs.ctypes.data, ve.ctypes.data)
+    if n < 0:
+        return n
+    return vs[:n], ve[:n]
+
+
+class OrDevCols(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("voff_base", C.c_uint64)] + [
+        (k, C.c_void_p) for k in ("voffset", "key", "rec_off", "ubuf")] + [("ubuf_len", C.c_uint64)] + [
+        (k, C.c_void_p) for k in ("block_size", "ref_id", "pos", "l_read_name", "mapq", "bin", "n_cigar",
+                                  "flag", "l_seq", "next_ref_id", "next_pos", "tlen", "layout_ok",
+                                  "name_off", "cigar_off", "seq_off", "aux_off", "names", "cigars",
+                                  "seq", "qual", "aux")]
+
+
+class OrCheck(C.Structure):
+    _fields_ = [("n_checked", C.c_uint64), ("mismatches", C.c_uint64), ("first_bad", C.c_int64),
+                ("bad_field", C.c_int32), ("status", C.c_int32)]
+
+
+CHECK_FIELDS = {1: "count", 2: "voffset", 3: "key", 4: "fixed", 5: "record bytes", 6: "layout_ok",
+                7: "names", 8: "cigars", 9: "seq", 10: "qual", 11: "aux"}
+
+
+def check_whole(data, own_len, n_ref, dev, voff_base, n_splits, threads):
+    """Every record of one device decode checked against the oracle (test infrastructure:
+    bench.py's at-size parity).  `data` is the compressed window the device decoded, its
+    FileSplit [0, own_len): the device's FileVirtualSplit is [guess(0), own_len << 16 | 0xffff).
+    `dev` is an OrDevCols over the decode's host copy, record i at index i, voffsets = window
+    voffsets + voff_base.  The oracle's own guess of 0 must be the device's first record; the
+    sequential read is then cut at the device's voffsets of every (n / n_splits)-th record, and
+    the pieces are read by the oracle's BAMRecordReader one per thread and compared record by
+    record with the device records (C, or_check_split).  A piece that starts at a device voffset
+    that is not a true record start, or a device record missing or extra, shows up as a count
+    or voffset mismatch of the piece before it, so the pieces tile the read exactly."""
+    import threading
+    a, p = _buf(data)
+    n = int(dev.n)
+    out = {"shard_records": n, "records_checked": 0}
+    g, err = guess_bam_record_start(a, 0, own_len, n_ref)
+    dvo = np.ctypeslib.as_array(C.cast(dev.voffset, C.POINTER(C.c_uint64)), shape=(n,)) \
+        if n else np.zeros(0, np.uint64)
+    if err or g == own_len or not n or int(dvo[0]) != g + voff_base:
+        out["error"] = "first record: oracle guess %d (err %d), device %s" % (
+            g, err, int(dvo[0]) - voff_base if n else None)
+        return out
+    S = max(1, min(n_splits, n))
+    idx = np.array([n * k // S for k in range(S + 1)], np.int64)
+    vs = [int(dvo[idx[k]]) - voff_base for k in range(S)]
+    ve = vs[1:] + [(own_len << 16) | 0xffff]
+    outs = [OrCheck() for _ in range(S)]
+    L = lib()
+
+    def work(k):
+        L.or_check_split(p, len(a), vs[k], ve[k], n_ref, C.addressof(dev), int(idx[k]), C.addressof(outs[k]))
+
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(S)]
+    for k in range(0, S, max(1, threads)):
+        for th in ths[k:k + threads]:
+            th.start()
+        for th in ths[k:k + threads]:
+            th.join()
+    short = [k for k in range(S) if int(outs[k].n_checked) != int(idx[k + 1] - idx[k])]
+    bad = [k for k in range(S) if outs[k].mismatches]
+    out.update({
+        "records_checked": int(sum(min(int(o.n_checked), int(idx[k + 1] - idx[k])) for k, o in enumerate(outs))),
+        "pieces": S, "pieces_with_wrong_count": len(short),
+        "mismatches": int(sum(o.mismatches for o in outs)) + len(short),
+        "oracle_status": sorted(set(int(o.status) for o in outs)),
+        "first_bad": ({"record": int(outs[bad[0]].first_bad),
+                       "field": CHECK_FIELDS.get(int(outs[bad[0]].bad_field), "?")} if bad else
+                      {"record": int(idx[short[0]]), "field": "count"} if short else None)})
+    return out
+
+
 def splitting_index(data, granularity=4096):
     a, p = _buf(data)
     cap = 1 << 20
@@ -246,6 +335,15 @@ _REC_DT = np.dtype([("block_size", "<i4"), ("ref_id", "<i4"), ("pos", "<i4"),
                     ("l_read_name", "u1"), ("mapq", "u1"), ("bin", "<u2"), ("n_cigar", "<u2"),
                     ("flag", "<u2"), ("l_seq", "<i4"), ("next_ref_id", "<i4"), ("next_pos", "<i4"),
                     ("tlen", "<i4")])
+
+
+def record_fixed_bytes(cols, idx):
+    """the 36 fixed bytes (block_size .. tlen) of records idx of a read_split result: (k, 36) u8"""
+    idx = np.asarray(idx, np.int64)
+    fixed = np.zeros(len(idx), _REC_DT)
+    for f in _REC_DT.names:
+        fixed[f] = cols[f][idx]
+    return fixed.view(np.uint8).reshape(len(idx), 36)
 
 
 def record_payloads(cols):

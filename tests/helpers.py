@@ -172,3 +172,65 @@ def regroup_bam(data, text_fn, rg_fn, ref_fn=None):
         out.append(struct.pack("<i", len(body)) + bytes(body))
         i += 1
     return np.frombuffer(bgzf_pack(b"".join(out)), np.uint8).copy()
+
+
+def reheader_bam(data, text_fn=None, refs_fn=None):
+    """A copy of a BAM with its header rewritten: text_fn(text) -> new text, refs_fn(refs) -> new
+    binary dictionary [(name bytes incl. anything after whitespace, l_ref)] (crafted-header tests
+    of SAMHeaderReader / [htsjdk] BAMFileReader.readHeader); the records are kept as they are.
+    A name given as (raw bytes, l_name) writes that l_name (e.g. 1: an empty name)."""
+    import struct
+    u = bam_stream(data)
+    lt = struct.unpack_from("<i", u, 4)[0]
+    text = u[8:8 + lt]
+    p = 8 + lt
+    n = struct.unpack_from("<i", u, p)[0]
+    p += 4
+    refs = []
+    for _ in range(n):
+        ln = struct.unpack_from("<i", u, p)[0]
+        refs.append((u[p + 4:p + 3 + ln], struct.unpack_from("<i", u, p + 4 + ln)[0]))
+        p += 8 + ln
+    text = text_fn(text) if text_fn else text
+    refs = refs_fn(refs) if refs_fn else refs
+    out = [b"BAM\x01", struct.pack("<i", len(text)), text, struct.pack("<i", len(refs))]
+    for nm, ln in refs:
+        if isinstance(nm, tuple):
+            raw, l_name = nm
+            out += [struct.pack("<i", l_name), raw]
+        else:
+            out += [struct.pack("<i", len(nm) + 1), nm, b"\0"]
+        out.append(struct.pack("<i", ln))
+    out.append(u[p:])
+    return np.frombuffer(bgzf_pack(b"".join(out)), np.uint8).copy()
+
+
+def _sq_edit(k, fn):
+    """text_fn editing the k-th @SQ line with fn(line) -> line"""
+    def ed(text):
+        lines = text.split(b"\n")
+        idx = [i for i, ln in enumerate(lines) if ln.startswith(b"@SQ")]
+        lines[idx[k]] = fn(lines[idx[k]])
+        return b"\n".join(lines)
+    return ed
+
+
+# crafted headers: (label, text_fn, refs_fn, accepted by the reader?)
+CRAFTED_HEADERS = [
+    ("as_is", None, None, True),
+    ("name_mismatch", None, lambda r: [(b"chrX" if i == 3 else nm, ln) for i, (nm, ln) in enumerate(r)], False),
+    ("length_mismatch", None, lambda r: [(nm, ln + 1 if i == 7 else ln) for i, (nm, ln) in enumerate(r)], False),
+    ("empty_name", None, lambda r: [((b"\0", 1) if i == 2 else nm, ln) for i, (nm, ln) in enumerate(r)], False),
+    ("count_mismatch", None, lambda r: r[:-1], False),
+    ("binary_name_cut_at_whitespace", None,
+     lambda r: [(nm + b" extra words" if i == 4 else nm, ln) for i, (nm, ln) in enumerate(r)], True),
+    ("no_sq_in_text", lambda t: b"\n".join(ln for ln in t.split(b"\n") if not ln.startswith(b"@SQ")), None, True),
+    ("no_sq_in_text_any_binary", lambda t: b"\n".join(ln for ln in t.split(b"\n") if not ln.startswith(b"@SQ")),
+     lambda r: [(b"zz" + nm, 7) for nm, _ in r], True),
+    ("sq_without_ln", None, None, False),  # text_fn set below
+    ("sq_ln_not_an_int", None, None, False),
+    ("crlf_lines", lambda t: t.replace(b"\n", b"\r\n"), None, True),
+]
+CRAFTED_HEADERS[8] = ("sq_without_ln", _sq_edit(1, lambda ln: b"\t".join(
+    f for f in ln.split(b"\t") if not f.startswith(b"LN:"))), None, False)
+CRAFTED_HEADERS[9] = ("sq_ln_not_an_int", _sq_edit(0, lambda ln: ln.replace(b"LN:", b"LN:x")), None, False)

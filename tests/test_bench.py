@@ -39,6 +39,10 @@ def test_bench_spawns_two_ranks_gloo():
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "shard2"
     assert res["parity"]["mismatches"] == 0 and res["parity"]["splits"] == 4
     assert res["value"] > 0
+    # every record of each rank's timed launch against the oracle
+    assert len(res["parity"]["whole_launch"]) == 2
+    for w in res["parity"]["whole_launch"]:
+        assert w["mismatches"] == 0 and w["records_checked"] == w["shard_records"] > 0, w
     # config #5's leg across the ranks (tools/sort_leg.py), here over the host-staged gloo exchange
     srt = res["sort"]
     assert srt["parity"]["mismatches"] == 0, srt
@@ -67,3 +71,41 @@ def test_bench_config4_windows(gpus, extra):
     assert p["records_checked_vs_body_decode"] == res["config"]["records_all_gpus"]
     if gpus == 1:
         assert res["config"]["windows_per_step_rank0"] > 1
+
+
+def test_sort_leg_budget_from_the_whole_run_deadline():
+    """The Sort leg's watchdog counts from process start (--deadline), not from the leg's start,
+    so a hung exchange ends while the driver's own limit still leaves time to print the line."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.sort_leg_budget(420.0, 100.0) == 320.0
+    assert bench.sort_leg_budget(420.0, 420.0 - bench.SORT_LEG_MIN_S) == bench.SORT_LEG_MIN_S
+    assert bench.sort_leg_budget(420.0, 400.0) == 0.0  # too little left: the leg is skipped
+    assert bench.sort_leg_budget(420.0, 500.0) == 0.0
+
+
+_HANG = r"""
+import json, sys, time, types
+sys.path.insert(0, %r)
+import bench
+bench.SORT_LEG_MIN_S = 0.5
+fake = types.ModuleType("sort_leg")
+fake.run = lambda *a, **k: time.sleep(600)  # an exchange that never returns
+sys.modules["sort_leg"] = fake
+args = types.SimpleNamespace(deadline=time.time() - bench.T_START + 1.5, sort_size=1, seed=0, sort_steps=1)
+res = {"value": 1.0}
+bench.guarded_sort_leg(None, None, 0, 2, args, 1, None, None, res)
+print("not reached")
+"""
+
+
+def test_sort_leg_watchdog_prints_the_line_and_exits_nonzero():
+    """A hung Sort leg: rank 0 prints the headline line carrying the leg's timeout, and the
+    process exits with WATCHDOG_EXIT (3), so launchers see the failure."""
+    r = subprocess.run([sys.executable, "-c", _HANG % ROOT], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and "not reached" not in r.stdout
+    res = json.loads(lines[0])
+    assert res["value"] == 1.0 and "timeout" in res["sort"]["error"]

@@ -837,6 +837,72 @@ def test_records_to_host_is_what_the_reader_hands_out(gpu_ctx, oracle_mod, name)
         assert d2h <= 1.1 * len(pay)
 
 
+def test_two_readers_interleaved_on_one_context(gpu_ctx, oracle_mod):
+    """Two drop-in readers sharing one context (formats.context() hands every reader of a device
+    the same one), stepped alternately: each window's host copy lives in its own stream's staging
+    (hbam_split_records_to_host), so a window still in use is never overwritten — or freed — by
+    the other reader's next window.  Both readers' records equal the oracle's."""
+    a_data, b_data = _load("small_pe.bam"), _load("edge_uniform_long.bam")
+    want = {}
+    for tag, data in (("a", a_data), ("b", b_data)):
+        h = oracle_mod.read_header(data)
+        ref = oracle_mod.read_split(data, h["first_voffset"], _whole(data))
+        want[tag] = (ref, oracle_mod.record_payloads(ref)[0].tobytes(), h)
+    # b's windows grow (one window, then larger ones) so its staging is re-allocated mid-way
+    gens = {tag: gpu_ctx.split_stream(data, want[tag][2]["first_voffset"], _whole(data), want[tag][2]["n_ref"],
+                                      window_bytes=(48 << 10) if tag == "a" else (96 << 10), host="records")
+            for tag, data in (("a", a_data), ("b", b_data))}
+    got = {"a": [], "b": []}
+    held = {}
+    live = ["a", "b"]
+    while live:
+        for tag in list(live):
+            w = next(gens[tag], None)
+            if w is None:
+                live.remove(tag)
+                continue
+            other = "b" if tag == "a" else "a"
+            if other in held:  # the other reader's window, read AFTER this reader's new window
+                ow = held.pop(other)
+                got[other].append((ow["key"].copy(), ow["ubuf"][:].tobytes()))
+            held[tag] = w
+    for tag, w in held.items():
+        got[tag].append((w["key"].copy(), w["ubuf"][:].tobytes()))
+    for tag in ("a", "b"):
+        ref, pay, _ = want[tag]
+        assert np.array_equal(np.concatenate([k for k, _ in got[tag]]), ref["key"]), tag
+        assert b"".join(u for _, u in got[tag]) == pay, tag
+    assert len(got["a"]) > 3 and len(got["b"]) > 1
+
+
+def test_records_to_host_refuses_permuted_columns(gpu_ctx):
+    """hbam_records_to_host copies the byte range of a decoded split's records; columns whose
+    records are not back to back in index order (a permutation) are refused with HBAM_EINVAL
+    instead of copying the wrong range."""
+    import ctypes as C
+    import torch
+    from hadoop_bam import _lib
+    data = _load("small_pe.bam")
+    d = torch.from_numpy(data).cuda()
+    h = gpu_ctx.parse_header(d)
+    rc, cols = gpu_ctx.decode_split_device(d, h["first_voffset"], _whole(data), h["n_ref"])
+    assert rc == 0 and cols.n_records > 10
+    out = _lib.Columns()
+    assert gpu_ctx.L.hbam_records_to_host(gpu_ctx.h, C.byref(cols), C.byref(out)) == 0
+    n = int(cols.n_records)
+    ro = torch.empty(n, dtype=torch.int64, device="cuda")
+    # records 3 and 5 swapped: the first and last stay, so only the contiguity check can see it
+    perm = torch.arange(n, dtype=torch.int32, device="cuda")
+    perm[3], perm[5] = 5, 3
+    torch.cuda.synchronize()
+    assert gpu_ctx.L.hbam_permute(gpu_ctx.h, C.cast(cols.rec_off, C.c_void_p), 8, C.c_void_p(perm.data_ptr()),
+                                  n, C.c_void_p(ro.data_ptr())) == 0
+    torch.cuda.synchronize()
+    cols.rec_off = C.cast(C.c_void_p(ro.data_ptr()), type(cols.rec_off))
+    assert gpu_ctx.L.hbam_records_to_host(gpu_ctx.h, C.byref(cols), C.byref(out)) == -11
+    assert "not contiguous" in gpu_ctx.last_error()
+
+
 def test_windowed_decode_comp_base(gpu_ctx, oracle_mod):
     """hbam_decode_split with comp_base != 0: a window [c, c+W) of the file decodes the same
     records as the whole buffer up to the window's EMORE, whose voffset[n] is the resume point."""
@@ -873,3 +939,26 @@ def test_guesses_across_launch_batches(oracle_mod, monkeypatch):
     for i in range(len(beg)):
         assert (int(out[i]), int(err[i])) == oracle_mod.guess_bam_record_start(
             data, int(beg[i]), int(end[i]), h["n_ref"]), i
+
+
+@pytest.mark.parametrize("label,text_fn,refs_fn,ok", __import__("helpers").CRAFTED_HEADERS,
+                         ids=[c[0] for c in __import__("helpers").CRAFTED_HEADERS])
+def test_header_dictionary_checks_on_device(gpu_ctx, oracle_mod, label, text_fn, refs_fn, ok):
+    """hbam_parse_header (device inflate, host parse) and every n_ref = -1 decode raise
+    SAMFormatException (HBAM_EFORMAT) exactly where the oracle's restatement of [htsjdk]
+    BAMFileReader.readHeader does (dictionary count / name / length mismatch, empty binary name,
+    @SQ without LN or with a non-integer LN) and accept the same headers with the same fields."""
+    from helpers import reheader_bam
+    data = reheader_bam(_load("small_pe.bam"), text_fn, refs_fn)
+    want = oracle_mod.read_header(data)
+    got = gpu_ctx.parse_header(data)
+    assert got == want, (label, got, want)
+    if ok:
+        ref = oracle_mod.read_split(data, want["first_voffset"], _whole(data))
+        dec = gpu_ctx.decode_split(data, want["first_voffset"], _whole(data), n_ref=-1)
+        assert dec["rc"] == 0, dec
+        assert_same_split(dec, ref)
+    else:
+        assert got == -3
+        dec = gpu_ctx.decode_split(data, 0, _whole(data), n_ref=-1)
+        assert dec["rc"] == -3, (label, dec.get("rc"))

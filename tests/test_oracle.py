@@ -231,3 +231,88 @@ def test_vectorised_pools_match_per_record_restatement(oracle_mod, name):
     a, b = oracle_mod.pools(r), oracle_pools(r)
     for k in ("layout_ok", "names", "cigars", "seq", "qual", "aux"):
         assert a[k].dtype == b[k].dtype and np.array_equal(a[k], b[k]), k
+
+
+def _fake_device_cols(oracle_mod, data, voff_base):
+    """A decode's host copy as the device path lays it out, built from the oracle's own read
+    (record bytes, pools and offsets) — input for the whole-output checker's self-test."""
+    h = oracle_mod.read_header(data)
+    cols = oracle_mod.read_split(data, h["first_voffset"], (len(data) << 16) | 0xffff)
+    pay, off = oracle_mod.record_payloads(cols)
+    pl = oracle_mod.pools(cols)
+    n = cols["n"]
+    vo = cols["var_off"].astype(np.int64)
+    L, nc, ls = (np.where(pl["layout_ok"] == 1, cols[k].astype(np.int64), 0) for k in ("l_read_name", "n_cigar", "l_seq"))
+    na = np.where(pl["layout_ok"] == 1, (vo[1:] - vo[:-1]) - (L + 4 * nc + (ls + 1) // 2 + ls), 0)
+
+    def offs(x):
+        o = np.zeros(n + 1, np.uint64)
+        o[1:] = np.cumsum(x)
+        return o
+    arrs = dict(voffset=cols["voffset"].astype(np.uint64) + np.uint64(voff_base), key=cols["key"],
+                rec_off=off[:-1].astype(np.uint64), ubuf=pay, layout_ok=pl["layout_ok"],
+                name_off=offs(L), cigar_off=offs(nc), seq_off=offs(ls), aux_off=offs(na),
+                names=pl["names"], cigars=pl["cigars"], seq=pl["seq"], qual=pl["qual"], aux=pl["aux"])
+    for k in ("block_size", "ref_id", "pos", "l_read_name", "mapq", "bin", "n_cigar", "flag", "l_seq",
+              "next_ref_id", "next_pos", "tlen"):
+        arrs[k] = cols[k]
+    arrs = {k: np.ascontiguousarray(v) if len(v) else np.zeros(1, v.dtype) for k, v in arrs.items()}
+    d = oracle_mod.OrDevCols()
+    d.n, d.voff_base, d.ubuf_len = n, voff_base, len(pay)
+    for k, v in arrs.items():
+        setattr(d, k, v.ctypes.data)
+    return d, arrs, h
+
+
+@pytest.mark.parametrize("name", ["small_pe.bam", "edge_uniform_long.bam", "edge_unsorted_l1.bam"])
+def test_whole_output_checker(oracle_mod, name):
+    """oracle.check_whole (bench.py's check of every record of the timed launch): a copy laid out
+    as the device's reports 0 mismatches and covers every record through many guessed splits;
+    one changed byte in any pool, the record bytes or a column is found at its record, and a
+    record missing from the copy is found by its piece's count."""
+    data = np.fromfile(os.path.join(GOLDEN, name), dtype=np.uint8)
+    base = 7 << 16
+    d, arrs, h = _fake_device_cols(oracle_mod, data, base)
+    r = oracle_mod.check_whole(data, len(data), h["n_ref"], d, base, 13, 4)
+    assert r["mismatches"] == 0 and r["first_bad"] is None, r
+    assert r["records_checked"] == d.n and r["pieces_with_wrong_count"] == 0, r
+    assert r["pieces"] == 13 and r["oracle_status"] == [0]
+    rng = np.random.default_rng(1)
+    for field, what in (("seq", "seq"), ("qual", "qual"), ("names", "names"), ("ubuf", "record bytes"),
+                        ("pos", "fixed"), ("key", "key"), ("aux", "aux")):
+        a = arrs[field]
+        if a.size < 2:
+            continue
+        i = int(rng.integers(0, a.size))
+        a.view(np.uint8)[i * a.itemsize] ^= 0x40
+        r = oracle_mod.check_whole(data, len(data), h["n_ref"], d, base, 13, 4)
+        a.view(np.uint8)[i * a.itemsize] ^= 0x40
+        assert r["mismatches"] >= 1 and r["first_bad"]["field"] == what, (field, r)
+    # a record dropped from the copy (every later record one index early)
+    d2, arrs2, _ = _fake_device_cols(oracle_mod, data, base)
+    d2.n = d.n - 1
+    for k in ("voffset", "key", "block_size", "ref_id", "pos", "l_read_name", "mapq", "bin", "n_cigar",
+              "flag", "l_seq", "next_ref_id", "next_pos", "tlen", "rec_off", "layout_ok"):
+        a = arrs2[k]
+        a[d.n // 2:-1] = a[d.n // 2 + 1:].copy()
+    r = oracle_mod.check_whole(data, len(data), h["n_ref"], d2, base, 13, 4)
+    assert r["mismatches"] >= 1 and r["records_checked"] < d.n, r
+
+
+@pytest.mark.parametrize("label,text_fn,refs_fn,ok", __import__("helpers").CRAFTED_HEADERS,
+                         ids=[c[0] for c in __import__("helpers").CRAFTED_HEADERS])
+def test_header_dictionary_checks(oracle_mod, label, text_fn, refs_fn, ok):
+    """SAMHeaderReader.readSAMHeaderFrom (SAMHeaderReader.java:53-72) -> [htsjdk] BAMFileReader
+    .readHeader / readSequenceRecord, restated (htsjdk absent: parity unpinned): with @SQ lines in
+    the text the binary dictionary must agree in count, per-entry name (binary name cut at its
+    first whitespace) and length; an empty binary name (l_name <= 1) and an @SQ line without LN or
+    with a non-integer LN raise SAMFormatException (OR_EFORMAT)."""
+    from helpers import reheader_bam
+    data = reheader_bam(np.fromfile(os.path.join(GOLDEN, "small_pe.bam"), np.uint8), text_fn, refs_fn)
+    h = oracle_mod.read_header(data)
+    if ok:
+        assert isinstance(h, dict), (label, h)
+        r = oracle_mod.read_split(data, h["first_voffset"], (len(data) << 16) | 0xffff)
+        assert r["status"] == 0 and r["n"] == 20000
+    else:
+        assert h == oracle_mod.OR_EFORMAT, (label, h)

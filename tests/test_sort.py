@@ -300,6 +300,61 @@ def test_rccl_exchange_one_rank_matches_oracle(gpu_ctx, oracle_mod, fname):
 
 
 @pytest.mark.gpu
+def test_sort_gather_and_exchange_above_2gib(gpu_ctx, oracle_mod):
+    """A sorted run whose payload offsets pass 2^31 (the regime of the round-5 readlane fault in
+    k_gather_records_tile: a 64-bit destination offset above 2^31 sign-extended) and its one-rank
+    RCCL exchange, whose payload goes out in several HBAM_XCHG_CHUNK (1 GiB) pieces.  Checked
+    against the oracle: keys in its total order, every payload offset, the payload of ~3,000
+    records (all of the last 1,000, where offsets exceed 2^31) byte for byte against the
+    oracle's record bytes, and a byte-sum over the whole payload; the exchange must hand back the
+    identical run."""
+    import torch
+    import genbam
+    from hadoop_bam import sort
+    data = np.asarray(genbam.generate(target_bytes=int(1.05e9), seed=11, sorted=0, threads=16))
+    cols = oracle_mod.read_split(data, oracle_mod.read_header(data)["first_voffset"],
+                                 (len(data) << 16) | 0xffff)
+    assert cols["status"] == 0
+    n = cols["n"]
+    o = oracle_mod.sort_order(cols["key"])
+    d = torch.from_numpy(data).cuda()
+    h = gpu_ctx.parse_header(d)
+    rc, dc = gpu_ctx.decode_split_device(d, h["first_voffset"], (len(data) << 16) | 0xffff, h["n_ref"])
+    assert rc == 0 and dc.status == 0 and int(dc.n_records) == n
+    ops = sort.HipSortOps(gpu_ctx)
+    run = ops.run_from_columns(dc)
+    assert np.array_equal(run.keys.cpu().numpy(), cols["key"][o])
+    want_v = cols["voffset"].astype(np.int64)[o]
+    assert np.array_equal(run.voffset.cpu().numpy(), want_v)
+    lens = 4 + cols["block_size"].astype(np.int64)[o]
+    off = run.offsets.cpu().numpy()
+    assert off[0] == 0 and np.array_equal(np.diff(off), lens)
+    assert off[-1] > (1 << 31) + (1 << 28), "payload must pass 2^31 well before its end"
+    pay = run.payload.cpu().numpy()
+    vo = cols["var_off"].astype(np.int64)
+    assert int(pay.sum(dtype=np.uint64)) == int(
+        cols["var"].sum(dtype=np.uint64) + oracle_mod.record_fixed_bytes(cols, np.arange(n)).sum(dtype=np.uint64))
+    rng = np.random.default_rng(5)
+    pick = np.unique(np.concatenate([rng.integers(0, n, 2000), np.arange(n - 1000, n)]))
+    fixed = oracle_mod.record_fixed_bytes(cols, o[pick])
+    for k, i in enumerate(pick):
+        j = int(o[i])
+        rec = pay[int(off[i]):int(off[i + 1])]
+        assert rec[:36].tobytes() == fixed[k].tobytes(), i
+        assert rec[36:].tobytes() == cols["var"][vo[j]:vo[j + 1]].tobytes(), i
+    comm = sort.RcclComm(gpu_ctx, 1, 0, sort.RcclComm.unique_id(gpu_ctx.L))
+    try:
+        ops2 = sort.HipSortOps(gpu_ctx, comm)
+        out = ops2.exchange_native(run, ops2.split_points_native(run))
+        assert out.n == n
+        assert torch.equal(out.keys, run.keys) and torch.equal(out.voffset, run.voffset)
+        assert torch.equal(out.offsets, run.offsets)
+        assert torch.equal(out.payload[:int(off[-1])], run.payload[:int(off[-1])])
+    finally:
+        comm.close()
+
+
+@pytest.mark.gpu
 def test_sort_received_after_async_device_op(gpu_ctx, oracle_mod):
     """sort_received's inputs produced by asynchronous torch work (pinned non_blocking copies
     and kernels still queued on torch's stream) must be complete before libhbam's own stream

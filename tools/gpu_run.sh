@@ -41,7 +41,7 @@ for spec in "$@"; do
     bench)
       timeout -k 10 600 python -u bench.py --steps ${a1:-20} --warmup 3 > $O/bench.json 2> $O/bench.err; r=$? ;;
     prof)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --parity-splits 0 > $O/bench_prof.json 2> $O/prof.err; r=$? ;;
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --parity-splits 0 --no-whole-check > $O/bench_prof.json 2> $O/prof.err; r=$? ;;
     pmc)  # pmc,COUNTERS[,SIZE[,LIB]]: one counter pass over a decode (csv per dispatch)
       P=$O/pmc_${a1//+/_}${a3:+_$a3}
       timeout -s KILL 300 rocprofv3 --pmc ${a1//+/ } -d $P -o run --output-format csv -- python3 tools/ab_decode.py --size ${a2:-2e9} --reps 1 --digest 0 --libs ${a3:-libhbam.so} > $P.txt 2>&1; r=$? ;;
