@@ -271,9 +271,10 @@ def whole_shard_check(ctx, cols, buf, own_len, off, threads):
     res["host_copy_s"] = round(t_copy, 2)
     res["seconds"] = round(time.time() - t, 2)
     res["what"] = ("every record of the timed launch (host copy of its output) vs the oracle's "
-                   "BAMRecordReader over the same split, cut into FileSplits aligned by the oracle's "
-                   "guesser: voffset, key, every fixed column, the record bytes and every lazy-getter "
-                   "pool (names, CIGAR, SEQ, QUAL, AUX, layout_ok), record by record")
+                   "BAMRecordReader over the same FileVirtualSplit (its start = the oracle's own guess), "
+                   "read in pieces cut at the device's voffsets, each piece required to end exactly where "
+                   "the next begins: voffset, key, every fixed column, the record bytes and every "
+                   "lazy-getter pool (names, CIGAR, SEQ, QUAL, AUX, layout_ok), record by record")
     return res, hc
 
 
