@@ -28,9 +28,8 @@
 
 using namespace hbam;
 
-#ifndef HBAM_GUESS_BATCH
-#define HBAM_GUESS_BATCH 16384  // guesses per launch (~66 KiB of scratch + the window cache each)
-#endif
+constexpr uint64_t GUESS_BATCH = 16384;  // guesses per launch (~66 KiB of scratch + the window cache
+                                         // each); env HBAM_GUESS_BATCH overrides (tests: multi-batch)
 
 namespace {
 
@@ -182,18 +181,17 @@ enum BufId {
 
 }  // namespace
 
-#ifndef HBAM_INFLATE_SLICES
-#define HBAM_INFLATE_SLICES 1  // A/B at 10 GB: 1 -> 163.4 ms, 2 -> 161.5, 4 -> 166.5, 8 -> 164.5 (Huffman + LZ77)
-#endif
-#define HBAM_MAX_SLICES 16
-#ifndef HBAM_WAVE_MAX_BLOCKS
+// inflate slices on two streams; A/B at 10 GB: 1 -> 163.4 ms, 2 -> 161.5, 4 -> 166.5, 8 -> 164.5
+// (Huffman + LZ77); env HBAM_INFLATE_SLICES overrides
+constexpr uint32_t INFLATE_SLICES = 1;
+constexpr uint32_t MAX_SLICES = 16;
 // Huffman pass by k_inflate_wave (a wave per block) for calls of up to this many BGZF blocks,
 // by k_inflate_tokens (a lane per block) above: the lane pass needs ~131k blocks (2 waves x 64
 // lanes x 1,024 SIMDs) to fill the chip, the wave pass fills it from a few thousand but costs
 // more per block.  Huffman ms, lane vs wave: 1 GB 16.8 / 9.5, 2 GB 20.8 / 18.2, 3 GB 21.5 / 27.0,
 // 5 GB 33.8 / 44.7, 10 GB 60 / 88.9 (profiles/r04/ab/huffman_wave_vs_lane_by_size.txt)
-#define HBAM_WAVE_MAX_BLOCKS 90000
-#endif
+// env HBAM_WAVE_MAX_BLOCKS overrides (tests, A/B)
+constexpr uint64_t WAVE_MAX_BLOCKS = 90000;
 struct hbam_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -202,13 +200,13 @@ struct hbam_ctx {
   Buf bufs[B_COUNT_ALL];
   hipStream_t stream2 = nullptr;  // LZ77 pass of slice s beside the Huffman pass of slice s+1
   hipEvent_t ev[16];
-  hipEvent_t slice_ev[HBAM_MAX_SLICES + 1];
-  uint32_t inflate_slices = HBAM_INFLATE_SLICES;  // env HBAM_INFLATE_SLICES overrides (A/B)
-  uint64_t wave_max_blocks = HBAM_WAVE_MAX_BLOCKS;  // env HBAM_WAVE_MAX_BLOCKS overrides (tests, A/B)
+  hipEvent_t slice_ev[MAX_SLICES + 1];
+  uint32_t inflate_slices = INFLATE_SLICES;  // env HBAM_INFLATE_SLICES overrides (A/B)
+  uint64_t wave_max_blocks = WAVE_MAX_BLOCKS;  // env HBAM_WAVE_MAX_BLOCKS overrides (tests, A/B)
   bool slices_forced = false;                     // ... and then applies to small calls too
   hbam_timing timing{};
   uint64_t* pinned_small = nullptr;  // host pinned scalars
-  uint64_t guess_batch = HBAM_GUESS_BATCH;  // env HBAM_GUESS_BATCH overrides (tests: multi-batch)
+  uint64_t guess_batch = GUESS_BATCH;  // env HBAM_GUESS_BATCH overrides (tests: multi-batch)
   uint8_t* rec_host = nullptr;  // hbam_records_to_host: pinned, grow-only
   size_t rec_host_cap = 0;
   std::vector<hbam_comm*> comms;  // communicators tied to this context (hbam_comm.hip)
@@ -503,11 +501,11 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   if ((rc = ensure(c, B_BITMAP, nb * BITMAP_WORDS, &bitmap))) return rc;
   if ((rc = ensure(c, B_TAILS, 2 * nb + 2, &tails))) return rc;
   if ((rc = ensure(c, B_EDGE, 32 * nb + 32, &edges))) return rc;
-  uint32_t* retry = nullptr;  // [HBAM_MAX_SLICES counters][nb block indices]
+  uint32_t* retry = nullptr;  // [MAX_SLICES counters][nb block indices]
   const bool wave = nb <= c->wave_max_blocks;
   if (wave) {
-    if ((rc = ensure(c, B_RETRY, nb + HBAM_MAX_SLICES, &retry))) return rc;
-    HIPCHK(c, hipMemsetAsync(retry, 0, HBAM_MAX_SLICES * 4, c->stream));
+    if ((rc = ensure(c, B_RETRY, nb + MAX_SLICES, &retry))) return rc;
+    HIPCHK(c, hipMemsetAsync(retry, 0, MAX_SLICES * 4, c->stream));
   }
   // Both passes are latency-bound at low occupancy (Huffman: 2 waves/SIMD; LZ77: a serial
   // walk per block), so the blocks are cut into slices and the LZ77 pass of slice s runs on a
@@ -516,7 +514,7 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
   // writes bytewise (edge merge / LZ77 write-back), never the other side's.
   uint32_t ns = c->inflate_slices;
   if (ns < 1) ns = 1;
-  if (ns > HBAM_MAX_SLICES) ns = HBAM_MAX_SLICES;
+  if (ns > MAX_SLICES) ns = MAX_SLICES;
   if (!c->slices_forced && nb < (uint64_t)ns * 8192) ns = 1;  // small calls: one slice
   if (nb < ns) ns = 1;
   if (nb) {
@@ -525,7 +523,7 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
       if (!n) continue;
       hipStream_t rs = ns > 1 ? c->stream2 : c->stream;
       if (wave) {
-        uint32_t* rl = retry + HBAM_MAX_SLICES + lo;
+        uint32_t* rl = retry + MAX_SLICES + lo;
         k_inflate_wave<<<(uint32_t)n, 64, 0, c->stream>>>(dcomp, blk + lo, uoff + lo, (uint32_t)n, ubuf,
                                                          bitmap + lo * BITMAP_WORDS, tails + 2 * lo,
                                                          edges + 32 * lo, st + lo, rl, retry + si);
@@ -547,17 +545,17 @@ int inflate_blocks(hbam_ctx* c, const uint8_t* dcomp, const BlockRec* blk, uint6
                                                   tails + 2 * lo, st + lo);
     }
     if (ns > 1) {
-      HIPCHK(c, hipEventRecord(c->slice_ev[HBAM_MAX_SLICES], c->stream2));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->slice_ev[HBAM_MAX_SLICES], 0));
+      HIPCHK(c, hipEventRecord(c->slice_ev[MAX_SLICES], c->stream2));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->slice_ev[MAX_SLICES], 0));
     }
   }
   HIPCHK(c, hipGetLastError());
   if (wave && nb && getenv("HBAM_WV_STATS")) {  // diagnostics: blocks the wave pass left to the lane pass
-    uint32_t cnt[HBAM_MAX_SLICES];
+    uint32_t cnt[MAX_SLICES];
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(cnt, retry, sizeof(cnt), hipMemcpyDeviceToHost));
     uint64_t tot = 0;
-    for (uint32_t si = 0; si < HBAM_MAX_SLICES; ++si) tot += cnt[si];
+    for (uint32_t si = 0; si < MAX_SLICES; ++si) tot += cnt[si];
     fprintf(stderr, "hbam: wave inflate left %llu of %llu blocks to the lane pass\n", (unsigned long long)tot,
             (unsigned long long)nb);
 #ifdef HBAM_WV_PROF

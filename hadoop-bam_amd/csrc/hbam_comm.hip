@@ -20,9 +20,7 @@
 #include <rccl/rccl.h>
 
 // largest single point-to-point transfer of the Sort exchange (bytes)
-#ifndef HBAM_XCHG_CHUNK
-#define HBAM_XCHG_CHUNK (1ull << 30)
-#endif
+constexpr uint64_t XCHG_CHUNK = 1ull << 30;
 
 namespace {
 
@@ -266,20 +264,20 @@ extern "C" int hbam_sort_exchange(hbam_ctx* c, hbam_comm* m, const hbam_sorted_r
       (rc = ensure(c, B_X_BS, nr + 1, &rs)) || (rc = ensure(c, B_X_PAY, nb + 1, &rp)))
     return rc;
   HIPCHK(c, hipEventRecord(c->ev[12], c->stream));
-  // every transfer goes out in pieces of at most HBAM_XCHG_CHUNK bytes: a peer's payload at config
+  // every transfer goes out in pieces of at most XCHG_CHUNK bytes: a peer's payload at config
   // #5 is several GB, and no single point-to-point call above 2 GiB has been exercised; both sides
   // cut a (sender, receiver) pair's bytes at the same offsets, and RCCL matches the pieces in order
   auto send = [&](const void* ptr, uint64_t bytes, int peer) -> ncclResult_t {
-    for (uint64_t o = 0; o < bytes; o += HBAM_XCHG_CHUNK) {
-      const ncclResult_t r = R.Send((const uint8_t*)ptr + o, std::min<uint64_t>(HBAM_XCHG_CHUNK, bytes - o),
+    for (uint64_t o = 0; o < bytes; o += XCHG_CHUNK) {
+      const ncclResult_t r = R.Send((const uint8_t*)ptr + o, std::min<uint64_t>(XCHG_CHUNK, bytes - o),
                                     ncclUint8, peer, m->comm, c->stream);
       if (r != ncclSuccess) return r;
     }
     return ncclSuccess;
   };
   auto recv = [&](void* ptr, uint64_t bytes, int peer) -> ncclResult_t {
-    for (uint64_t o = 0; o < bytes; o += HBAM_XCHG_CHUNK) {
-      const ncclResult_t r = R.Recv((uint8_t*)ptr + o, std::min<uint64_t>(HBAM_XCHG_CHUNK, bytes - o), ncclUint8,
+    for (uint64_t o = 0; o < bytes; o += XCHG_CHUNK) {
+      const ncclResult_t r = R.Recv((uint8_t*)ptr + o, std::min<uint64_t>(XCHG_CHUNK, bytes - o), ncclUint8,
                                     peer, m->comm, c->stream);
       if (r != ncclSuccess) return r;
     }

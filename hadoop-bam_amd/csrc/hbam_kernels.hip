@@ -77,10 +77,10 @@ __global__ __launch_bounds__(256) void k_scan_chunks(const uint8_t* __restrict__
   // each thread tests 16 consecutive positions per step using a 32-byte window
   // (requesting the next step's window before testing this one: 1.56 -> 1.71 ms at 5 GB,
   // profiles/r03/ab/scan_prefetch_5g.txt; not kept)
-#ifndef HBAM_SCAN_POS
-#define HBAM_SCAN_POS 32  // positions per thread per step: 16 -> 32 keeps twice the bytes in flight, 1.55 -> 1.40 ms at 5 GB (profiles/r04/ab/scan_32_positions_5g.txt)
-#endif
-  constexpr int SP = HBAM_SCAN_POS;
+// positions per thread per step: 16 -> 32 keeps twice the bytes in flight, 1.55 -> 1.40 ms at 5 GB
+// (profiles/r04/ab/scan_32_positions_5g.txt)
+constexpr int SCAN_POS = 32;
+  constexpr int SP = SCAN_POS;
   for (uint32_t step = 0; step < SCAN_CHUNK / (256 * SP); ++step) {
     const uint64_t p0 = c0 + ((uint64_t)step * 256 + threadIdx.x) * SP;
     if (p0 >= end) break;
@@ -239,7 +239,7 @@ __global__ void k_verify_chain(const uint8_t* __restrict__ comp, const uint64_t*
 
 // ------------------------------------------------------------------------------------
 // K2: inflate = two kernels.
-//  k_inflate_wave (phase 1, calls of up to HBAM_WAVE_MAX_BLOCKS blocks): one wave per BGZF
+//  k_inflate_wave (phase 1, calls of up to WAVE_MAX_BLOCKS blocks): one wave per BGZF
 //    block, same output; see inflate_wave.h.  Blocks it does not take go to k_inflate_tokens.
 //  k_inflate_tokens (phase 1): one lane per BGZF block (SIMT across blocks); Huffman
 //    decode with wave-uniform input epochs; literals land in ubuf, each match leaves a
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
 
 // Huffman pass, one wave (= one workgroup) per BGZF block; see inflate_wave.h.  Blocks it does
 // not take are appended to list for k_inflate_tokens.
-__global__ __launch_bounds__(64, HBAM_WV_WAVES) void k_inflate_wave(const uint8_t* __restrict__ comp,
+__global__ __launch_bounds__(64, WV_WAVES) void k_inflate_wave(const uint8_t* __restrict__ comp,
                                                                    const BlockRec* __restrict__ blk,
                                                                    const uint64_t* __restrict__ uoff,
                                                                    uint32_t nblk, uint8_t* __restrict__ ubuf,
@@ -512,9 +512,6 @@ __global__ __launch_bounds__(64) void k_block_entry(const uint8_t* __restrict__ 
   if (lane == 0) entry[b] = found;
 }
 
-#ifndef HBAM_WALK_BUF
-#define HBAM_WALK_BUF 1
-#endif
 // Walk block b from entry[b]: record starts in [uoff[b], uoff[b+1]) are stored as u16
 // offsets (cap WALK_CAP per block); exit[b] = first chain position >= uoff[b+1], or
 // CHAIN_STOP when a record cannot be framed (the chain ends there).
@@ -535,7 +532,6 @@ static __device__ void walk_one(const uint8_t* __restrict__ u, const uint64_t* _
     exitp[b] = CHAIN_STOP;
     return;
   }
-#if HBAM_WALK_BUF
   // The offsets go out eight at a time as one 16-byte store (WALK_CAP and the block's slot are
   // multiples of 8 entries): a 2-byte store per record from a lane per block reached L2 as a
   // partial line each time (WRITE_SIZE 2.41 GB for 0.15 GB of offsets at config #2).
@@ -555,14 +551,6 @@ static __device__ void walk_one(const uint8_t* __restrict__ u, const uint64_t* _
     const uint32_t idx = n - k + i, slot = 8u - k + i;
     if (idx < WALK_CAP) rb[idx] = (uint16_t)(slot < 4u ? lo >> (16u * slot) : hi >> (16u * (slot - 4u)));
   }
-#else
-  while (r < b1) {
-    if (n < WALK_CAP) rel[(uint64_t)b * WALK_CAP + n] = (uint16_t)(r - b0);
-    ++n;
-    r = fmt.next(u, r, hard_end);
-    if (r == CHAIN_STOP) break;
-  }
-#endif
   count[b] = n;
   exitp[b] = r;
 }
@@ -681,23 +669,21 @@ static __device__ __forceinline__ uint64_t ld_u64_unaligned(const uint8_t* p) {
 // and the tail as two 8-byte loads (masked): an unmapped read's hash (the whole variable part,
 // ~19 blocks) used to wait for one dependent load pair per block plus one per tail byte, and
 // with ~1 % unmapped reads about half of the waves carried one such lane.
-#ifndef HBAM_MH_BATCH
-#define HBAM_MH_BATCH 8
-#endif
+constexpr int32_t MH_BATCH = 8;  // 16-byte blocks of a murmur hash loaded together
 static __device__ uint64_t murmur3_java(const uint8_t* __restrict__ key, int32_t len) {
   const int32_t nblocks = len / 16;
   uint64_t h1 = 0, h2 = 0;
   const uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
-  for (int32_t i0 = 0; i0 < nblocks; i0 += HBAM_MH_BATCH) {
-    uint64_t kk[2 * HBAM_MH_BATCH];
+  for (int32_t i0 = 0; i0 < nblocks; i0 += MH_BATCH) {
+    uint64_t kk[2 * MH_BATCH];
 #pragma unroll
-    for (int32_t j = 0; j < HBAM_MH_BATCH; ++j) {
+    for (int32_t j = 0; j < MH_BATCH; ++j) {
       const uint8_t* q = key + 16 * (i0 + j < nblocks ? i0 + j : i0);  // past the last block: re-read one
       kk[2 * j] = ld_u64_unaligned(q);
       kk[2 * j + 1] = ld_u64_unaligned(q + 8);
     }
 #pragma unroll
-    for (int32_t j = 0; j < HBAM_MH_BATCH; ++j) {
+    for (int32_t j = 0; j < MH_BATCH; ++j) {
       if (i0 + j < nblocks) {
         uint64_t k1 = kk[2 * j], k2 = kk[2 * j + 1];
         k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
@@ -911,15 +897,14 @@ static __device__ __forceinline__ void seq8(uint32_t x, uint32_t& o0, uint32_t& 
 // with units, and a unit finds its record's rank as a popcount: the records whose first unit lies
 // in the 64-unit window are one bit each of a mask (distinct positions), the earlier ones are
 // counted by one ballot.  One ds_read_b128 per unit.
-#ifndef HBAM_POOLS_U
-#define HBAM_POOLS_U 4  // windows per step; A/B at 5 GB, pools ms: 1 9.34, 2 8.57, 3 8.88, 4 8.51
-#endif                  // (profiles/r05/ab/pools_windows_per_step_5g.txt; same pools in every build)
-static_assert(HBAM_POOLS_U >= 2 && HBAM_POOLS_U <= 4, "pools: 2-4 windows per step (the load asm below)");
+// windows per step; A/B at 5 GB, pools ms: 1 9.34, 2 8.57, 3 8.88, 4 8.51
+// (profiles/r05/ab/pools_windows_per_step_5g.txt; same pools in every build)
+constexpr uint32_t POOLS_U = 4;
 static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
   return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l) |
          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l) << 32;
 }
-// Record-major units (HBAM_POOLS_RM): the field-major loop below reads a tile's source lines once
+// Record-major units: the field-major loop below reads a tile's source lines once
 // per field, and a tile's source (64 records, ~22 KB) is evicted from the 4 MB L2 of an XCD (768
 // resident waves) before the next field comes to it — FETCH_SIZE counted 2.8 x U for that loop
 // (profiles/r05/pmc_kernels.json).  Here a tile's segments (record, field) are numbered in record
@@ -931,13 +916,6 @@ static __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
 // found the segment directly, five segment starts per lane in the window mask: 0.3-0.5 ms slower
 // at 5 GB, profiles/r05/ab/pools_record_level_mapping_5g.txt.)  Taken for tiles whose records
 // are all under 2^16 units (1 MiB); other tiles take the field-major loop.
-#ifndef HBAM_POOLS_RM
-#define HBAM_POOLS_RM 1
-#endif
-#ifndef HBAM_POOLS_BACK
-#define HBAM_POOLS_BACK 1
-#endif
-#if HBAM_POOLS_RM
 static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__ u, const DevColumns& c,
                                                       uint4* segs, uint64_t* pbt, uint32_t lane, uint64_t le,
                                                       uint64_t src, const uint32_t (&L)[5],
@@ -977,13 +955,13 @@ static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   const uint8_t* const sbase = u + sb;
-  for (uint32_t q0 = 0; q0 < T; q0 += 64 * HBAM_POOLS_U) {
-    u32x4_t raw[HBAM_POOLS_U];
-    const uint8_t* sp[HBAM_POOLS_U];
-    uint8_t* dp[HBAM_POOLS_U];
-    uint32_t nn[HBAM_POOLS_U], fs[HBAM_POOLS_U];
+  for (uint32_t q0 = 0; q0 < T; q0 += 64 * POOLS_U) {
+    u32x4_t raw[POOLS_U];
+    const uint8_t* sp[POOLS_U];
+    uint8_t* dp[POOLS_U];
+    uint32_t nn[POOLS_U], fs[POOLS_U];
 #pragma unroll
-    for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
+    for (uint32_t w = 0; w < POOLS_U; ++w) {
       nn[w] = 0;
       fs[w] = 0;
       dp[w] = (uint8_t*)sbase;  // (never stored through: nn = 0)
@@ -1006,33 +984,20 @@ static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__
         const uint4 S = segs[64u + 5u * rk + f];
         const uint32_t j = dq - S.w, len = S.y;
         uint32_t n = len - 16u * j;
-#if HBAM_POOLS_BACK
         const uint32_t sbk = (n < 16u && len >= 16u && (f != 2u || (n & 1u) == 0u)) ? 16u - n : 0u;
         n += sbk;
-#else
-        const uint32_t sbk = 0u;
-#endif
         nn[w] = n;
         dp[w] = (uint8_t*)(uintptr_t)pbt[f] + S.x + 16u * j - sbk;
         sp[w] = sbase + A.y + S.z + (f == 2u ? 8u * j - sbk / 2u : 16u * j - sbk);
         fs[w] = f;
       }
     }
-#if HBAM_POOLS_U == 2
-    asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off\n\ts_waitcnt vmcnt(0)"
-                 : "=&v"(raw[0]), "=&v"(raw[1]) : "v"(sp[0]), "v"(sp[1]) : "memory");
-#elif HBAM_POOLS_U == 3
-    asm volatile("global_load_dwordx4 %0, %3, off\n\tglobal_load_dwordx4 %1, %4, off\n\t"
-                 "global_load_dwordx4 %2, %5, off\n\ts_waitcnt vmcnt(0)"
-                 : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]) : "v"(sp[0]), "v"(sp[1]), "v"(sp[2]) : "memory");
-#else
     asm volatile("global_load_dwordx4 %0, %4, off\n\tglobal_load_dwordx4 %1, %5, off\n\t"
                  "global_load_dwordx4 %2, %6, off\n\tglobal_load_dwordx4 %3, %7, off\n\ts_waitcnt vmcnt(0)"
                  : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]), "=&v"(raw[3])
                  : "v"(sp[0]), "v"(sp[1]), "v"(sp[2]), "v"(sp[3]) : "memory");
-#endif
 #pragma unroll
-    for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
+    for (uint32_t w = 0; w < POOLS_U; ++w) {
       if (q0 + 64u * w >= T) break;  // wave-uniform
       u32x4_a1 v = u32x4_a1{raw[w][0], raw[w][1], raw[w][2], raw[w][3]};
       if (__ballot(fs[w] == 2u) != 0ull) {  // a SEQ unit in the window: 8 packed bytes -> 16 chars
@@ -1051,14 +1016,11 @@ static __device__ __forceinline__ void pools_tile_rm(const uint8_t* __restrict__
     }
   }
 }
-#endif
 __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict__ u, uint64_t nrec,
                                                        const uint64_t* __restrict__ rec_off,
                                                        DevColumns c) {
-  __shared__ uint4 s_recs[4][HBAM_POOLS_RM ? 384 : 64];
-#if HBAM_POOLS_RM
+  __shared__ uint4 s_recs[4][384];
   __shared__ uint64_t s_pb[4][8];
-#endif
   const uint32_t lane = threadIdx.x & 63u;
   uint4* const recs = s_recs[threadIdx.x >> 6];
   const uint64_t ntiles = (nrec + 63) / 64;
@@ -1079,7 +1041,6 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
       o_seq = c.seq_off[r];
       o_aux = c.aux_off[r];
     }
-#if HBAM_POOLS_RM
     {
       const uint32_t L[5] = {nl, 4u * nc, ls, ls, na};
       const uint64_t d[5] = {o_name, 4 * o_cig, o_seq, o_seq, o_aux};
@@ -1095,7 +1056,6 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
         continue;
       }
     }
-#endif
 #pragma unroll 1
     for (uint32_t f = 0; f < 5; ++f) {
       uint32_t len;
@@ -1120,7 +1080,7 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
       asm volatile("" ::: "memory");  // (one wave: its LDS operations run in issue order)
       uint8_t* const dbase = base + db;
       const uint8_t* const sbase = u + sb;
-      // HBAM_POOLS_U windows per step, their loads issued back to back before any store.  With
+      // POOLS_U windows per step, their loads issued back to back before any store.  With
       // one window per step the compiler puts s_waitcnt vmcnt(0) ahead of each load (the address
       // is built by VALU writes into registers that held the last store's data, which the store
       // reads late), so every step paid a load round trip plus a store acknowledgement.  The U
@@ -1128,13 +1088,13 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
       // dummy address): nothing the compiler schedules can touch the destinations between a load
       // and its data (a wait in a separate statement let it copy the registers before the data
       // had landed), and no load is left in flight after the statement.
-      for (uint32_t q0 = 0; q0 < total; q0 += 64 * HBAM_POOLS_U) {
-        u32x4_t raw[HBAM_POOLS_U];
-        const uint8_t* sp[HBAM_POOLS_U];
-        uint8_t* dp[HBAM_POOLS_U];
-        uint32_t nn[HBAM_POOLS_U];
+      for (uint32_t q0 = 0; q0 < total; q0 += 64 * POOLS_U) {
+        u32x4_t raw[POOLS_U];
+        const uint8_t* sp[POOLS_U];
+        uint8_t* dp[POOLS_U];
+        uint32_t nn[POOLS_U];
 #pragma unroll
-        for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
+        for (uint32_t w = 0; w < POOLS_U; ++w) {
           nn[w] = 0;
           dp[w] = dbase;
           sp[w] = sbase;
@@ -1155,21 +1115,12 @@ __global__ __launch_bounds__(256) void k_decode_pools(const uint8_t* __restrict_
             sp[w] = sbase + rr.x + (f == 2 ? 8u : 16u) * k;
           }
         }
-#if HBAM_POOLS_U == 2
-        asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off\n\ts_waitcnt vmcnt(0)"
-                     : "=&v"(raw[0]), "=&v"(raw[1]) : "v"(sp[0]), "v"(sp[1]) : "memory");
-#elif HBAM_POOLS_U == 3
-        asm volatile("global_load_dwordx4 %0, %3, off\n\tglobal_load_dwordx4 %1, %4, off\n\t"
-                     "global_load_dwordx4 %2, %5, off\n\ts_waitcnt vmcnt(0)"
-                     : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]) : "v"(sp[0]), "v"(sp[1]), "v"(sp[2]) : "memory");
-#else
         asm volatile("global_load_dwordx4 %0, %4, off\n\tglobal_load_dwordx4 %1, %5, off\n\t"
                      "global_load_dwordx4 %2, %6, off\n\tglobal_load_dwordx4 %3, %7, off\n\ts_waitcnt vmcnt(0)"
                      : "=&v"(raw[0]), "=&v"(raw[1]), "=&v"(raw[2]), "=&v"(raw[3])
                      : "v"(sp[0]), "v"(sp[1]), "v"(sp[2]), "v"(sp[3]) : "memory");
-#endif
 #pragma unroll
-        for (uint32_t w = 0; w < HBAM_POOLS_U; ++w) {
+        for (uint32_t w = 0; w < POOLS_U; ++w) {
           if (q0 + 64u * w >= total) break;  // wave-uniform
           u32x4_a1 v;
           if (f == 2) {

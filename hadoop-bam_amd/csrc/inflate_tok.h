@@ -11,7 +11,7 @@
 // the 64 is always refilling and the wait is per wave.  Here the input moves in wave-uniform
 // epochs instead:
 //   * each lane holds 32 compressed bytes in two register banks plus a 64-bit bit buffer;
-//   * every HBAM_TOK_K iterations (the same iteration for every active lane) a lane merges
+//   * every TOK_K iterations (the same iteration for every active lane) a lane merges
 //     the 16-byte quad it requested at the previous epoch into a free bank and requests the
 //     next one, so a load has a whole epoch to land before anything waits on it;
 //   * a lane that would need more bits than its banks hold skips the iteration (stall) until
@@ -44,10 +44,7 @@ namespace hbam {
 #define TOK_PC(i) (void)0
 #endif
 
-#ifndef HBAM_TOK_K
-#define HBAM_TOK_K 4  // symbol-loop iterations per input epoch (power of two)
-#endif
-constexpr uint32_t TOK_K = HBAM_TOK_K;
+constexpr uint32_t TOK_K = 4;  // symbol-loop iterations per input epoch (power of two)
 
 // The fast path (tok_fast_spec): up to two literals and a match per iteration, decoded first
 // (both lit/len lookups before either LDS symbol read), then written as one packet

@@ -37,22 +37,12 @@
 
 namespace hbam {
 
-#ifndef HBAM_WV_R
-#define HBAM_WV_R 10  // lit/len root bits
-#endif
-#ifndef HBAM_WV_DR
-#define HBAM_WV_DR 8  // distance root bits
-#endif
-#ifndef HBAM_WV_TBL
-#define HBAM_WV_TBL 3072  // u16 table entries per wave: lit/len root + long, distance root + long
-#endif
-#ifndef HBAM_WV_WARM
-#define HBAM_WV_WARM 256  // bits a lane decodes before its range to fall into step
-#endif
-#ifndef HBAM_WV_WAVES
-#define HBAM_WV_WAVES 5  // waves per SIMD asked of the register allocator (96 VGPRs, no spills; 4: 19.0 ms, 5: 18.2 ms at 2 GB)
-#endif
-constexpr uint32_t WV_R = HBAM_WV_R, WV_DR = HBAM_WV_DR, WV_TBL = HBAM_WV_TBL, WV_WARM = HBAM_WV_WARM;
+constexpr uint32_t WV_R = 10;     // lit/len root bits
+constexpr uint32_t WV_DR = 8;     // distance root bits
+constexpr uint32_t WV_TBL = 3072; // u16 table entries per wave: lit/len root + long, distance root + long
+constexpr uint32_t WV_WARM = 256; // bits a lane decodes before its range to fall into step
+// waves per SIMD asked of the register allocator (96 VGPRs, no spills; 4: 19.0 ms, 5: 18.2 ms at 2 GB)
+constexpr uint32_t WV_WAVES = 5;
 constexpr uint32_t WV_MINSEG = 512;   // bits per lane range at least
 constexpr uint32_t WV_STAGE = 128;    // stream words staged in LDS for the header decode
 constexpr uint32_t WV_TOK_BITS = 64;  // one iteration: 15 + 15 + 5 + 15 + 13 bits

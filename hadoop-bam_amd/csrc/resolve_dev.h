@@ -24,18 +24,15 @@
 
 namespace hbam {
 
-#ifndef HBAM_RS_W
-// A/B at 2 GB (stretch 2 KiB): 4096 -> 20.0 ms, 2048 -> 18.0, 1024 -> 16.7; at 10 GB with packed
-// match records and 8 waves/SIMD (HBAM_RS_WAVES): 1024 -> 48.8 ms (LDS caps it at 7 waves), 512 ->
-// 42.6 ms (profiles/r02/s2/ab_resolve_occupancy_10g.txt); 0 is not supported
-#define HBAM_RS_W 512
-#endif
-#ifndef HBAM_RS_S
-#define HBAM_RS_S 1024  // A/B at 2 GB (window 1 KiB): 2048 -> 16.8 ms, 1024 -> 11.7 ms; k_resolve_units needs 1024
-#endif
-constexpr uint32_t RS_S = HBAM_RS_S;                  // stretch (output bytes): 1024 or 2048
+// window kept in LDS behind the stretch.  A/B at 2 GB (stretch 2 KiB): 4096 -> 20.0 ms, 2048 ->
+// 18.0, 1024 -> 16.7; at 10 GB with packed match records and 8 waves/SIMD: 1024 -> 48.8 ms (LDS
+// caps it at 7 waves), 512 -> 42.6 ms (profiles/r02/s2/ab_resolve_occupancy_10g.txt); with the
+// units kernel at 5 GB: 512 15.4, 1 KiB 16.3, 2 KiB 17.0 ms (profiles/r05/ab/resolve_window_*)
+constexpr uint32_t RS_W = 512;
+// stretch (output bytes).  A/B at 2 GB (window 1 KiB): 2048 -> 16.8 ms, 1024 -> 11.7 ms;
+// k_resolve_units' unit records need 1 KiB
+constexpr uint32_t RS_S = 1024;
 constexpr uint32_t RS_C = RS_S / 1024;                // 16-byte columns per lane per stretch
-constexpr uint32_t RS_W = HBAM_RS_W;                  // window kept in LDS behind the stretch
 constexpr uint32_t RS_BUF = RS_W + 2 * RS_S + 48;     // + pad for 32-byte over-reads
 static_assert(RS_W >= 16 && RS_W % 16 == 0 && (RS_S == 1024 || RS_S == 2048),
               "window: whole 16-byte columns; stretch: 1 or 2 KiB (one or two columns per lane)");

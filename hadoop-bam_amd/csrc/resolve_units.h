@@ -130,11 +130,9 @@ __device__ __forceinline__ void ru_copy(uint8_t* __restrict__ buf, uint32_t di, 
   else ru_put(buf, di, n, v);
 }
 
-#ifndef HBAM_RU_WAVES
-#define HBAM_RU_WAVES 8
-#endif
+constexpr uint32_t RU_WAVES = 8;  // waves per SIMD (the LDS allows 8 at 4.9 KiB per block)
 
-__global__ __launch_bounds__(64, HBAM_RU_WAVES) void k_resolve_units(const BlockRec* __restrict__ blk,
+__global__ __launch_bounds__(64, RU_WAVES) void k_resolve_units(const BlockRec* __restrict__ blk,
                                                                      const uint64_t* __restrict__ uoff, uint32_t nblk,
                                                                      uint8_t* __restrict__ ubuf,
                                                                      const uint32_t* __restrict__ bitmap,
