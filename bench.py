@@ -592,7 +592,8 @@ def headline(args, world, elapsed, stages, huff_ms, ubytes, n_rec, own_len, file
     # the newest committed PMC pass of this kernel over the same workload (tools/pmc_summarize.py)
     huff_kernel = "k_inflate_wave" if nblk <= WAVE_MAX_BLOCKS else "k_inflate_tokens"
     pmc_files = ((("r04", "round4-wave", "pmc_huffman.json"),) if huff_kernel == "k_inflate_wave" else
-                 (("r05", "round5", "pmc_k_inflate_tokens.json"), ("r04", "round4", "pmc_k_inflate_tokens.json")))
+                 (("r06", "round6", "pmc_k_inflate_tokens.json"), ("r05", "round5", "pmc_k_inflate_tokens.json"),
+                  ("r04", "round4", "pmc_k_inflate_tokens.json")))
     for rnd, tree, fname in pmc_files:
         pmc = os.path.join(ROOT, "profiles", rnd, fname)
         if traffic is None and os.path.exists(pmc):

@@ -51,7 +51,7 @@ for spec in "$@"; do
       if [ $r -eq 0 ]; then
         COMP=$(grep -m1 '^comp_bytes' $O/pmcb_fetch.txt | cut -d' ' -f2)
         STG=""; [ -s $O/bench.json ] && STG=$O/bench.json
-        python3 tools/pmc_summarize.py $(ls $O/pmcb_fetch/*counter_collection.csv $O/pmcb_fetch/*/*counter_collection.csv 2>/dev/null | head -1) $(ls $O/pmcb_write/*counter_collection.csv $O/pmcb_write/*/*counter_collection.csv 2>/dev/null | head -1) $COMP $O/pmcsum ${PMC_TREE:-round5} $STG > $O/pmcsum.txt 2>&1
+        python3 tools/pmc_summarize.py $(ls $O/pmcb_fetch/*counter_collection.csv $O/pmcb_fetch/*/*counter_collection.csv 2>/dev/null | head -1) $(ls $O/pmcb_write/*counter_collection.csv $O/pmcb_write/*/*counter_collection.csv 2>/dev/null | head -1) $COMP $O/pmcsum ${PMC_TREE:-round6} $STG > $O/pmcsum.txt 2>&1
       fi ;;
     bin)  # bin,PATH: a probe executable of the repository
       timeout -k 10 300 ./$a1 > $O/$(basename $a1).txt 2>&1; r=$? ;;
