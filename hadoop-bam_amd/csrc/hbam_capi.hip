@@ -1248,11 +1248,18 @@ extern "C" int hbam_decode_split(hbam_ctx* c, const uint8_t* comp, int on_device
   }
   // ---- pools
   uint64_t tot_name = 0, tot_cig = 0, tot_seq = 0, tot_aux = 0;
-  // the four pool scans, their totals read back in one round trip
-  if ((rc = scan_exclusive<uint32_t>(c, dc.name_len, n_final, dc.name_off, nullptr))) return rc;
-  if ((rc = scan_exclusive<uint32_t>(c, dc.cigar_n, n_final, dc.cigar_off, nullptr))) return rc;
-  if ((rc = scan_exclusive<uint32_t>(c, dc.seq_len, n_final, dc.seq_off, nullptr))) return rc;
-  if ((rc = scan_exclusive<uint32_t>(c, dc.aux_len, n_final, dc.aux_off, nullptr))) return rc;
+  // the four pool scans in one pass (k_scan4_*), their totals read back in one round trip
+  {
+    const uint32_t tiles = (uint32_t)std::max<uint64_t>(1, (n_final + SCAN4_TILE - 1) / SCAN4_TILE);
+    uint64_t* partial;
+    if ((rc = ensure(c, B_PARTIAL, 4ull * tiles + 1, &partial))) return rc;
+    const Scan4In in{{dc.name_len, dc.cigar_n, dc.seq_len, dc.aux_len}};
+    const Scan4Out so{{dc.name_off, dc.cigar_off, dc.seq_off, dc.aux_off}};
+    k_scan4_reduce<<<tiles, 256, 0, c->stream>>>(in, n_final, partial, tiles);
+    k_scan4_partials<<<4, 256, 0, c->stream>>>(partial, tiles, so, n_final);
+    k_scan4_apply<<<tiles, 256, 0, c->stream>>>(in, n_final, partial, tiles, so);
+    HIPCHK(c, hipGetLastError());
+  }
   {
     const uint64_t* offs[4] = {dc.name_off, dc.cigar_off, dc.seq_off, dc.aux_off};
     for (int q = 0; q < 4; ++q)

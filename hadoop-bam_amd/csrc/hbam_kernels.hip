@@ -1212,6 +1212,134 @@ __global__ __launch_bounds__(SCAN_WG) void k_scan_apply(const T* __restrict__ in
 }
 
 // explicit instantiations used by the runtime
+// ---- the four pool-length scans at once (names, CIGAR, SEQ/QUAL, AUX: u32 -> u64 exclusive)
+// Three launches for the four arrays instead of twelve, and a thread takes 16 consecutive
+// elements of each array (four 16-byte loads) with the block scan on registers and one LDS pass
+// instead of k_scan_apply's sixteen LDS Hillis-Steele rounds per tile.  The arrays hold n + 16
+// readable elements (fill_columns: n + 1 plus the 64-byte pad), so a tile's tail needs no guard on
+// its loads, only on the values.
+constexpr uint32_t SCAN4_PER = 16, SCAN4_TILE = 256u * SCAN4_PER;
+struct Scan4In {
+  const uint32_t* a[4];
+};
+struct Scan4Out {
+  uint64_t* o[4];
+};
+static __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
+    v += (uint64_t)hi << 32 | lo;
+  }
+  return v;
+}
+static __device__ __forceinline__ void scan4_load(const uint32_t* __restrict__ a, uint64_t e0, uint64_t n,
+                                                  uint32_t (&v)[SCAN4_PER]) {
+  const bool any = e0 < n;  // a thread past the end loads nothing
+#pragma unroll
+  for (uint32_t k = 0; k < SCAN4_PER; k += 4) {
+    const uint4 q = any ? *(const uint4*)(a + e0 + k) : make_uint4(0, 0, 0, 0);
+    v[k] = e0 + k < n ? q.x : 0u;
+    v[k + 1] = e0 + k + 1 < n ? q.y : 0u;
+    v[k + 2] = e0 + k + 2 < n ? q.z : 0u;
+    v[k + 3] = e0 + k + 3 < n ? q.w : 0u;
+  }
+}
+__global__ __launch_bounds__(256) void k_scan4_reduce(Scan4In in, uint64_t n, uint64_t* __restrict__ partial,
+                                                      uint32_t tiles) {
+  __shared__ uint64_t s[4][4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const uint64_t e0 = (uint64_t)blockIdx.x * SCAN4_TILE + (uint64_t)tid * SCAN4_PER;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t v[SCAN4_PER];
+    scan4_load(in.a[q], e0, n, v);
+    uint64_t t = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN4_PER; ++k) t += v[k];
+    t = wave_sum_u64(t);
+    if (lane == 0) s[q][w] = t;
+  }
+  __syncthreads();
+  if (tid < 4) partial[(uint64_t)tid * tiles + blockIdx.x] = s[tid][0] + s[tid][1] + s[tid][2] + s[tid][3];
+}
+// one workgroup per array: exclusive scan of its tile sums in place; out[n] = the array's total
+__global__ __launch_bounds__(256) void k_scan4_partials(uint64_t* __restrict__ partial, uint32_t tiles,
+                                                        Scan4Out out, uint64_t n) {
+  __shared__ uint64_t s[4];
+  const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  uint64_t* p = partial + (uint64_t)q * tiles;
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < tiles; b0 += 256) {
+    const uint32_t j = b0 + tid;
+    const uint64_t v = j < tiles ? p[j] : 0;
+    uint64_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t lo = __shfl_up((uint32_t)incl, o), hi = __shfl_up((uint32_t)(incl >> 32), o);
+      if ((int)lane >= o) incl += (uint64_t)hi << 32 | lo;
+    }
+    if (lane == 63) s[w] = incl;
+    __syncthreads();
+    uint64_t wb = 0;
+    for (uint32_t k = 0; k < w; ++k) wb += s[k];
+    const uint64_t tot = s[0] + s[1] + s[2] + s[3];
+    if (j < tiles) p[j] = carry + wb + incl - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (tid == 0) out.o[q][n] = carry;
+}
+__global__ __launch_bounds__(256) void k_scan4_apply(Scan4In in, uint64_t n, const uint64_t* __restrict__ partial,
+                                                     uint32_t tiles, Scan4Out out) {
+  __shared__ uint64_t s[4][4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const uint64_t e0 = (uint64_t)blockIdx.x * SCAN4_TILE + (uint64_t)tid * SCAN4_PER;
+  uint64_t base[4], tt[4];
+  uint32_t v[4][SCAN4_PER];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    scan4_load(in.a[q], e0, n, v[q]);
+    uint64_t t = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN4_PER; ++k) t += v[q][k];
+    uint64_t incl = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t lo = __shfl_up((uint32_t)incl, o), hi = __shfl_up((uint32_t)(incl >> 32), o);
+      if ((int)lane >= o) incl += (uint64_t)hi << 32 | lo;
+    }
+    if (lane == 63) s[q][w] = incl;
+    tt[q] = incl - t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint64_t wb = partial[(uint64_t)q * tiles + blockIdx.x];
+    for (uint32_t k = 0; k < w; ++k) wb += s[q][k];
+    base[q] = wb + tt[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint64_t run = base[q];
+    uint64_t r[SCAN4_PER];
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN4_PER; ++k) {
+      r[k] = run;
+      run += v[q][k];
+    }
+    uint64_t* o = out.o[q] + e0;
+    if (e0 + SCAN4_PER <= n) {
+#pragma unroll
+      for (uint32_t k = 0; k < SCAN4_PER; k += 2) *(ulonglong2*)(o + k) = make_ulonglong2(r[k], r[k + 1]);
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < SCAN4_PER; ++k)
+        if (e0 + k < n) o[k] = r[k];
+    }
+  }
+}
+
 template __global__ void k_scan_reduce<uint32_t>(const uint32_t*, uint64_t, uint64_t*);
 template __global__ void k_scan_apply<uint32_t>(const uint32_t*, uint64_t, const uint64_t*, uint64_t*);
 
