@@ -297,7 +297,8 @@ __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t*
 #endif
     // per-lane symbol tables, lane-contiguous (dword-interleaving them across the lanes removes
     // the LDS bank conflicts, 75 % of the pass's LDS cycles, but not time: 33.7 vs 34.3 ms at
-    // 5 GB, profiles/r03/ab/huffman_interleaved_symtab_5g.txt)
+    // 5 GB, profiles/r03/ab/huffman_interleaved_symtab_5g.txt; re-measured on the round-6 pass:
+    // 30.9 / 30.9 -> 31.0 / 31.2 ms, profiles/r06/ab/huffman_interleaved_symtab_5g.txt)
     uint8_t* const my_ll = s_ll + threadIdx.x * 288;
     uint8_t* const my_d = s_d + threadIdx.x * 32;
     st = inflate_tokens_block(comp + r.coff + 18, r.clen - 26u, r.isize, my_ll, my_d,

@@ -60,7 +60,7 @@ def main():
         P = pbuf.view(-1, 32)[:nb].cpu().numpy().astype(np.float64)
         R = P[:, 16:24]
         tot = R.sum()
-        names = ["epoch/stall", "litlen lookup", "literal", "len extra", "distance", "match emit",
+        names = ["epoch", "symbol loop", "loop latch", "len extra", "distance", "match emit",
                  "header", "slow path"]
         print("Huffman pass, %d blocks, %.3g cycles summed over lanes" % (nb, tot))
         for i, nm in enumerate(names):
