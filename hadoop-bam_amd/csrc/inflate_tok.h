@@ -53,15 +53,7 @@ constexpr uint32_t TOK_K = 4;  // symbol-loop iterations per input epoch (power 
 // (profiles/r02/s2/ab_spec_10g.txt).
 // stream bits one fast-path iteration may consume: 2 lit/len codes + length extra + distance
 // code + distance extra = 15+15+5+15+13 = 63 (<= 64)
-#ifndef HBAM_TOK_3L
-#define HBAM_TOK_3L 0
-#endif
-#if HBAM_TOK_3L
-// three lit/len codes + length extra + distance code + distance extra = 45+5+15+13 = 78
-constexpr uint32_t TOK_FAST_BITS = 80u;
-#else
 constexpr uint32_t TOK_FAST_BITS = 64u;
-#endif
 constexpr uint32_t TOK_LENS_LL = 32;    // lens scratch: lit/len code lengths at +32 ..
 constexpr uint32_t TOK_LENS_D = 320;    //               distance code lengths at +320 (<= 30)
 
@@ -644,95 +636,6 @@ __device__ __forceinline__ uint32_t tok_fast_spec(EIn& in, const HuffP& hl, cons
   ex = (domatch && n < mlen) ? 2u : ex;
   return ex;
 }
-#if HBAM_TOK_3L
-// Three lit/len slots per iteration: a literal, a literal, then a literal or the match (tokens of
-// the lane's stream: 48.3 M iterations instead of 58.1 M over 5,000 blocks of the generated data,
-// tools/lane_sim.c).  The bit buffer is topped up after the first code, so the second and third
-// lookups run on the same 64 bits (like the first two of tok_fast_spec); the three symbol reads
-// are in flight together.
-__device__ __forceinline__ uint32_t tok_fast3(EIn& in, const HuffP& hl, const HuffP& hd,
-                                              const uint8_t* __restrict__ syms_ll,
-                                              const uint8_t* __restrict__ syms_d, TSink& sink,
-                                              uint32_t& op, uint32_t isize, TPend& pd) {
-  ein_refill_sel(in);
-  uint32_t L1, idx1, hi1 = 0, L2, idx2, hi2 = 0, L3, idx3, hi3 = 0;
-  const bool ok1 = huffp_lookup<true>(hl, ein_rev15(in), L1, idx1, hi1);
-  const uint32_t sym1 = (uint32_t)syms_ll[ok1 ? idx1 : 0u] | hi1;
-  uint32_t ex = ok1 ? 0u : 3u;
-  ein_drop(in, ok1 ? L1 : 0u);
-  ein_refill_sel(in);
-  const bool ok2 = huffp_lookup<true>(hl, ein_rev15(in), L2, idx2, hi2);
-  const uint32_t l2 = ok2 ? L2 : 0u;
-  const uint32_t v3 = __builtin_bitreverse32((uint32_t)(in.bb >> l2)) >> 17;
-  const bool ok3 = huffp_lookup<true>(hl, v3, L3, idx3, hi3);
-  const uint32_t sym2 = (uint32_t)syms_ll[ok2 ? idx2 : 0u] | hi2;
-  const uint32_t sym3 = (uint32_t)syms_ll[ok3 ? idx3 : 0u] | hi3;
-  sink.put(pd.op1, pd.P, pd.nb);  // the previous iteration's packet
-  const bool lit1 = ok1 && hi1 == 0u;
-  ex = (ex == 0u && lit1 && op == isize) ? 2u : ex;
-  const bool emit1 = ex == 0u && lit1;
-  const uint32_t op1 = op;
-  op += emit1 ? 1u : 0u;
-  ex = (emit1 && !ok2) ? 3u : ex;
-  ein_drop(in, (emit1 && ok2) ? L2 : 0u);
-  const bool lit2 = emit1 && ok2 && hi2 == 0u;
-  ex = (ex == 0u && lit2 && op == isize) ? 2u : ex;
-  const bool emit2 = ex == 0u && lit2;
-  op += emit2 ? 1u : 0u;
-  ex = (emit2 && !ok3) ? 3u : ex;
-  ein_drop(in, (emit2 && ok3) ? L3 : 0u);
-  const bool lit3 = emit2 && ok3 && hi3 == 0u;
-  ex = (ex == 0u && lit3 && op == isize) ? 2u : ex;
-  const bool emit3 = ex == 0u && lit3;
-  op += emit3 ? 1u : 0u;
-  const uint32_t m = !emit1 ? sym1 : !emit2 ? sym2 : sym3;
-  const bool ism = ex == 0u && !emit3 && !lit3 && !(emit1 && lit2 && !emit2);
-  ex = (ism && m == 256u) ? 1u : ex;
-  ex = (ism && m > 285u) ? 3u : ex;
-  const bool dom = ism && m > 256u && m <= 285u;
-  uint32_t lbase, lext;
-  length_base_sel(dom ? m : 257u, lbase, lext);
-  ein_refill_sel(in);
-  lext = dom ? lext : 0u;
-  const uint32_t mlen = lbase + ein_peek(in, lext);
-  ein_drop(in, lext);
-  uint32_t L, idx, dh;
-  const bool okd = huffp_lookup<false>(hd, ein_rev15(in), L, idx, dh);
-  const uint32_t dsym = syms_d[okd ? idx : 0u];
-  sink.mark_if(pd.em, pd.opm);  // the previous iteration's match mark
-  ex = (dom && !okd) ? 3u : ex;
-  ein_drop(in, (dom && okd) ? L : 0u);
-  ex = (dom && okd && dsym > 29u) ? 3u : ex;
-  const bool dom2 = dom && ex == 0u;
-  uint32_t dbase, dext;
-  dist_base_sel(dom2 ? dsym : 0u, dbase, dext);
-  dext = dom2 ? dext : 0u;
-  const uint32_t dist = dbase + ein_peek(in, dext);
-  ein_drop(in, dext);
-  ex = (dom2 && op == isize) ? 2u : ex;
-  ex = (dom2 && ex == 0u && dist > op) ? 3u : ex;
-  const bool domatch = dom2 && ex == 0u;
-  uint32_t n = isize - op;
-  n = mlen < n ? mlen : n;
-  const bool last = domatch && n < 3u;  // the output filled up inside the match: last token
-  sink.t0 = last ? (op | n << 16 | 0x80000000u) : sink.t0;
-  sink.t1 = last ? dist : sink.t1;
-  const bool em = domatch && n >= 3u;
-  uint64_t P = emit1 ? (uint64_t)(sym1 & 0xffu) : 0ull;
-  P |= emit2 ? (uint64_t)(sym2 & 0xffu) << 8 : 0ull;
-  P |= emit3 ? (uint64_t)(sym3 & 0xffu) << 16 : 0ull;
-  const uint32_t nl = (emit1 ? 1u : 0u) + (emit2 ? 1u : 0u) + (emit3 ? 1u : 0u);
-  P |= em ? (uint64_t)((n - 3u) | (dist - 1u) << 8) << (8u * nl) : 0ull;
-  pd.op1 = op1;
-  pd.P = P;
-  pd.nb = nl + (em ? 3u : 0u);
-  pd.em = em;
-  pd.opm = op;
-  op += domatch ? n : 0u;
-  ex = (domatch && n < mlen) ? 2u : ex;
-  return ex;
-}
-#endif
 // One symbol with every zlib outcome checked (the stream's last 64 bits).
 __device__ __forceinline__ uint32_t tok_careful(EIn& in, const HuffP& hl, const HuffP& hd,
                                                 const uint8_t* __restrict__ syms_ll,
@@ -957,11 +860,7 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
 #endif
         const bool run = ex == 0u && !ein_short(in, TOK_FAST_BITS);
         const bool fast = in.total - in.consumed >= TOK_FAST_BITS;
-#if HBAM_TOK_3L
-        if (run && fast) ex = tok_fast3(in, hl, hd, syms_ll, syms_d, sink, op, isize, pd);
-#else
         if (run && fast) ex = tok_fast_spec(in, hl, hd, syms_ll, syms_d, sink, op, isize, pd);
-#endif
         if (__builtin_amdgcn_ballot_w64(run && !fast) != 0u) {
           if (run && !fast) {
             pd.flush(sink);
