@@ -256,6 +256,7 @@ __device__ unsigned long long* g_prof = nullptr;
 #define PROF_CLK() __builtin_amdgcn_s_memtime()
 #define PROF_RT() __builtin_amdgcn_s_memrealtime()
 #endif
+static_assert(TOK_LENS_END == LENS_SLOT, "k_inflate_tokens: code-length scratch size");
 __global__ __launch_bounds__(INFLATE_WG, 2) void k_inflate_tokens(const uint8_t* __restrict__ comp,
                                                                   const BlockRec* __restrict__ blk,
                                                                   const uint64_t* __restrict__ uoff,

@@ -56,6 +56,7 @@ constexpr uint32_t TOK_K = 4;  // symbol-loop iterations per input epoch (power 
 constexpr uint32_t TOK_FAST_BITS = 64u;
 constexpr uint32_t TOK_LENS_LL = 32;    // lens scratch: lit/len code lengths at +32 ..
 constexpr uint32_t TOK_LENS_D = 320;    //               distance code lengths at +320 (<= 30)
+constexpr uint32_t TOK_LENS_END = 352;  // = LENS_SLOT (hbam_internal.h)
 
 // ---- input: two register banks + one quad in flight ------------------------------------
 typedef const __attribute__((address_space(1))) u32x4_t* gq_ptr;  // global (not flat) loads
@@ -772,53 +773,77 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
           if (!tok_build(lens, 19, syms_ll, t, 0)) { rc = INF_DATA; goto done; }
           hc = t;
         }
-        // lit/len lengths -> lens[32 ..], distance lengths -> lens[320 ..]
+#ifdef HBAM_PROF
+        TOK_PT(3);  // header bits + the code-length table
+#endif
+        // lit/len lengths -> lens[32 ..], distance lengths -> lens[320 ..].  The scratch is zeroed
+        // first (20 quads), so a run of zero lengths (codes 17 / 18, up to 138 each) only advances
+        // `have`; the loop is wave-uniform with the symbol loop's epoch clock (a per-lane clock put
+        // an epoch, whose vmcnt(0) also waits for the last length's store, in nearly every
+        // iteration of the divergent loop).
         const uint32_t total = nlen + ndist;
+        {
+          uint4* l4 = (uint4*)(lens + TOK_LENS_LL);
+#pragma unroll
+          for (int q = 0; q < (int)((TOK_LENS_END - TOK_LENS_LL) / 16u); ++q) l4[q] = make_uint4(0, 0, 0, 0);
+        }
         uint32_t have = 0;
         uint32_t prev = 0;
-        while (have < total) {
-          if ((++it & (TOK_K - 1u)) == 0u) ein_epoch(in);
-          if (ein_short(in, 14)) continue;  // stall
-          ein_refill(in);
-          uint32_t L, sym;
-          if (hc.empty) {
-            L = 1;
-            sym = 0;
-            if (ein_avail(in) < 1u) goto leave;
-          } else {
-            int32_t idx;
-            const uint32_t v = ein_rev15(in);
-            huff_lookup(hc, v, L, idx);  // CODES sets are complete
-            if (L > ein_avail(in)) goto leave;
-            sym = syms_ll[idx];
+        uint32_t hx = 0;  // 0 go on, 2 leave (zlib stops), 3 data error
+        for (;;) {
+          if ((__builtin_amdgcn_readfirstlane(++it) & (TOK_K - 1u)) == 0u) ein_epoch(in);
+          const bool act = hx == 0u && have < total;
+          if (__builtin_amdgcn_ballot_w64(act) == 0u) break;
+          if (act && !ein_short(in, 14)) {
+            ein_refill(in);
+            uint32_t L = 1, sym = 0;
+            if (hc.empty) {
+              hx = ein_avail(in) < 1u ? 2u : 0u;
+            } else {
+              int32_t idx;
+              huff_lookup(hc, ein_rev15(in), L, idx);  // CODES sets are complete
+              if (L > ein_avail(in)) hx = 2u;
+              else sym = syms_ll[idx];
+            }
+            if (hx == 0u) {
+              if (sym < 16u) {
+                ein_drop(in, L);
+                lens[have < nlen ? TOK_LENS_LL + have : TOK_LENS_D + (have - nlen)] = (uint8_t)sym;
+                ++have;
+                prev = sym;
+              } else {
+                const uint32_t xb = sym == 16u ? 2u : sym == 17u ? 3u : 7u;
+                if (L + xb > ein_avail(in)) {
+                  hx = 2u;
+                } else {
+                  ein_drop(in, L);
+                  if (sym == 16u && have == 0u) {
+                    hx = 3u;
+                  } else {
+                    const uint32_t rep = sym == 16u ? 3u + ein_peek(in, 2) : sym == 17u ? 3u + ein_peek(in, 3)
+                                                                                        : 11u + ein_peek(in, 7);
+                    ein_drop(in, xb);
+                    if (have + rep > total) {
+                      hx = 3u;
+                    } else {
+                      if (sym == 16u)  // a repeat of the previous length (3-6); zeros are already there
+                        for (uint32_t k = 0; k < rep; ++k)
+                          lens[have + k < nlen ? TOK_LENS_LL + have + k : TOK_LENS_D + (have + k - nlen)] = (uint8_t)prev;
+                      else
+                        prev = 0;
+                      have += rep;
+                    }
+                  }
+                }
+              }
+            }
           }
-          if (sym < 16u) {
-            ein_drop(in, L);
-            lens[have < nlen ? TOK_LENS_LL + have : TOK_LENS_D + (have - nlen)] = (uint8_t)sym;
-            ++have;
-            prev = sym;
-            continue;
-          }
-          const uint32_t xb = sym == 16u ? 2u : sym == 17u ? 3u : 7u;
-          if (L + xb > ein_avail(in)) goto leave;
-          ein_drop(in, L);
-          uint32_t rep;
-          uint32_t v8 = 0;
-          if (sym == 16u) {
-            if (have == 0) { rc = INF_DATA; goto done; }
-            v8 = prev;
-            rep = 3u + ein_peek(in, 2);
-          } else if (sym == 17u) {
-            rep = 3u + ein_peek(in, 3);
-          } else {
-            rep = 11u + ein_peek(in, 7);
-          }
-          ein_drop(in, xb);
-          if (have + rep > total) { rc = INF_DATA; goto done; }
-          for (uint32_t k = 0; k < rep; ++k, ++have)
-            lens[have < nlen ? TOK_LENS_LL + have : TOK_LENS_D + (have - nlen)] = (uint8_t)v8;
-          prev = v8;
         }
+        if (hx == 2u) goto leave;
+        if (hx == 3u) { rc = INF_DATA; goto done; }
+#ifdef HBAM_PROF
+        TOK_PT(4);  // the code lengths
+#endif
         if (lens[TOK_LENS_LL + 256] == 0) { rc = INF_DATA; goto done; }
         {
           Huff t;
@@ -827,6 +852,9 @@ __device__ __forceinline__ int32_t inflate_tokens_block(const uint8_t* __restric
           if (!tok_build(lens + TOK_LENS_D, (int)ndist, syms_d, t, 2)) { rc = INF_DATA; goto done; }
           huffp_make(t, hd);
         }
+#ifdef HBAM_PROF
+        TOK_PT(5);  // the lit/len and distance tables
+#endif
       } else {
         rc = INF_DATA;  // invalid block type
         goto done;

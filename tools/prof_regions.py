@@ -60,8 +60,8 @@ def main():
         P = pbuf.view(-1, 32)[:nb].cpu().numpy().astype(np.float64)
         R = P[:, 16:24]
         tot = R.sum()
-        names = ["epoch", "symbol loop", "loop latch", "len extra", "distance", "match emit",
-                 "header", "slow path"]
+        names = ["epoch", "symbol loop", "loop latch", "hdr+CL table", "code lengths", "LL+D tables",
+                 "drain", "slow path"]
         print("Huffman pass, %d blocks, %.3g cycles summed over lanes" % (nb, tot))
         for i, nm in enumerate(names):
             print("  %-14s %6.1f%%  %8.0f cyc/block" % (nm, 100 * R[:, i].sum() / tot, R[:, i].mean()))
