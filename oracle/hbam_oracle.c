@@ -1174,6 +1174,90 @@ void or_cols_free(or_cols* c) {
 }
 
 /* ------------------------------------------------------------------------------ */
+/* CPU baseline with the device path's whole output (bench.py cpu_baseline): the columns of
+ * or_read_split_cols plus the lazy getters' pools the device decode materialises (names, CIGAR
+ * u32s, SEQ as "=ACMGRSVTWYHKDBN" characters, QUAL, AUX, as check_one below defines them), built
+ * into growing host buffers per split.  Returns the status; *pool_bytes = the pools' total size. */
+typedef struct pools_ctx {
+  cols_ctx cx;
+  uint8_t* p;  /* one arena for the five pools (names | cigars | seq | qual | aux per record) */
+  uint64_t n, cap;
+  uint64_t* off; /* 5 offsets per record */
+  uint64_t ocap;
+} pools_ctx;
+
+static const char SEQ_ALPHA_B[] = "=ACMGRSVTWYHKDBN";
+
+static int pools_cb(void* user, const or_record* r) {
+  pools_ctx* x = (pools_ctx*)user;
+  if (cols_cb(&x->cx, r)) return 1;
+  const int64_t vlen = (int64_t)r->block_size - 32;
+  int64_t L = r->l_read_name, nc = r->n_cigar, ls = r->l_seq;
+  const int64_t fixed = L + 4 * nc + (ls + 1) / 2 + ls;
+  const int ok = ls >= 0 && fixed <= vlen;
+  const int64_t na = ok ? vlen - fixed : 0;
+  if (!ok) L = nc = ls = 0;
+  const uint64_t need = (uint64_t)(L + 4 * nc + 2 * ls + na);
+  if (x->n + need > x->cap) {
+    uint64_t ncap = x->cap ? x->cap * 2 : (1u << 22);
+    while (ncap < x->n + need) ncap *= 2;
+    uint8_t* np = (uint8_t*)realloc(x->p, ncap);
+    if (!np) { x->cx.oom = 1; return 1; }
+    x->p = np;
+    x->cap = ncap;
+  }
+  const uint64_t rec = x->cx.c->n - 1;
+  if (5 * (rec + 1) > x->ocap) {
+    uint64_t ncap = x->ocap ? x->ocap * 2 : 5 * 4096;
+    uint64_t* np = (uint64_t*)realloc(x->off, ncap * sizeof(uint64_t));
+    if (!np) { x->cx.oom = 1; return 1; }
+    x->off = np;
+    x->ocap = ncap;
+  }
+  const uint8_t* v = r->var;
+  uint8_t* d = x->p + x->n;
+  uint64_t* o = x->off + 5 * rec;
+  o[0] = x->n;
+  memcpy(d, v, (size_t)L);
+  o[1] = x->n + (uint64_t)L;
+  memcpy(d + L, v + L, (size_t)(4 * nc));
+  const uint8_t* sp = v + L + 4 * nc;
+  uint8_t* ds = d + L + 4 * nc;
+  o[2] = x->n + (uint64_t)(L + 4 * nc);
+  for (int64_t k = 0; k < ls; ++k) ds[k] = (uint8_t)SEQ_ALPHA_B[(k & 1) ? (sp[k >> 1] & 15) : (sp[k >> 1] >> 4)];
+  const uint8_t* qp = sp + (ls + 1) / 2;
+  o[3] = o[2] + (uint64_t)ls;
+  memcpy(ds + ls, qp, (size_t)ls);
+  o[4] = o[3] + (uint64_t)ls;
+  memcpy(ds + 2 * ls, qp + ls, (size_t)na);
+  x->n += need;
+  return 0;
+}
+
+int or_read_split_pools(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                        uint64_t* n_records, uint64_t* record_bytes, uint64_t* pool_bytes) {
+  or_cols c;
+  memset(&c, 0, sizeof c);
+  pools_ctx x;
+  memset(&x, 0, sizeof x);
+  x.cx.c = &c;
+  or_read_result res;
+  if (n_ref < 0)
+    or_read_split(f, len, v_start, v_end, 0, pools_cb, &x, &res);
+  else
+    read_split_body(f, len, v_start, v_end, 0, n_ref, pools_cb, &x, &res);
+  uint64_t rb = 0;
+  for (uint64_t i = 0; i < c.n; ++i) rb += (uint64_t)c.block_size[i] + 4u;
+  *n_records = c.n;
+  *record_bytes = rb;
+  *pool_bytes = x.n;
+  free(x.p);
+  free(x.off);
+  or_cols_free(&c);
+  return x.cx.oom ? OR_ENOMEM : res.status;
+}
+
+/* ------------------------------------------------------------------------------ */
 /* Whole-output checker (test infrastructure: bench.py's at-size parity).            */
 enum {
   CK_COUNT = 1, CK_VOFFSET, CK_KEY, CK_FIXED, CK_BYTES, CK_LAYOUT, CK_NAMES, CK_CIGARS, CK_SEQ,

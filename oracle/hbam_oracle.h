@@ -153,6 +153,11 @@ int or_read_split_cols(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_
 int or_read_split_cols_nref(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end,
                             int check_crc, int keep_var, int32_t n_ref, or_cols* out);
 void or_cols_free(or_cols* c);
+/* CPU baseline (bench.py): the same read with the columns AND the lazy getters' pools the device
+ * path materialises (names, CIGAR, SEQ characters, QUAL, AUX) built into host buffers, then freed.
+ * *record_bytes = sum of block_size + 4; *pool_bytes = the pools' size. */
+int or_read_split_pools(const uint8_t* f, uint64_t len, uint64_t v_start, uint64_t v_end, int32_t n_ref,
+                        uint64_t* n_records, uint64_t* record_bytes, uint64_t* pool_bytes);
 
 /* addProbabilisticSplits over a window of the file (a byte-range shard without the header):
  * the same as or_probabilistic_splits with the dictionary size given. */

@@ -62,6 +62,9 @@ def lib():
         L.or_read_split_cols.restype = C.c_int
         L.or_read_split_cols.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_int,
                                          C.POINTER(OrCols)]
+        L.or_read_split_pools.restype = C.c_int
+        L.or_read_split_pools.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int32,
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.or_probabilistic_splits_nref.restype = C.c_int64
         L.or_probabilistic_splits_nref.argtypes = [u8p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
                                                    C.c_int32, C.c_void_p, C.c_void_p]

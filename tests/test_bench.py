@@ -109,3 +109,34 @@ def test_sort_leg_watchdog_prints_the_line_and_exits_nonzero():
     assert len(lines) == 1 and "not reached" not in r.stdout
     res = json.loads(lines[0])
     assert res["value"] == 1.0 and "timeout" in res["sort"]["error"]
+
+
+def test_cpu_baseline_builds_the_same_pools_as_the_oracle_reader():
+    """bench.py's cpu_baseline does the device decode's whole work on host cores: every record of
+    its FileVirtualSplits with the lazy getters' pools built (or_read_split_pools), the same
+    records and pool bytes as oracle.read_split + oracle.pools over those splits."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for d in ("oracle", "tools", ""):
+        sys.path.insert(0, os.path.join(root, d))
+    import numpy as np
+    import bench
+    import genbam
+    import oracle
+    data = np.frombuffer(genbam.generate(records=20000, seed=11, odd_every=53), np.uint8)
+    r = bench.cpu_baseline(data, 0.02, 3)
+    assert r["status"] == [0] and r["kind"] == "port"
+    sample = int(min(len(data), 0.02 * 3 * 0.06e9))
+    block = int(np.ceil(sample / 3))
+    begs = list(range(0, sample, block))
+    ends = [min(b + block, sample) for b in begs]
+    base = np.ascontiguousarray(data[:sample + (1 << 20) if sample < len(data) else len(data)])
+    vs, ve = oracle.probabilistic_splits(base, np.array(begs, np.uint64), np.array(ends, np.uint64))
+    n = pb = 0
+    for a, b in zip(vs, ve):
+        c = oracle.read_split(base, int(a), int(b))
+        p = oracle.pools(c)
+        n += c["n"]
+        pb += sum(len(p[k]) * p[k].itemsize for k in ("names", "cigars", "seq", "qual", "aux"))
+    assert n > 0 and r["records_per_s"] > 0
+    assert r["pool_bytes"] == pb
+    assert ("%d records" % n) in r["sample"]
