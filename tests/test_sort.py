@@ -628,3 +628,52 @@ def test_multi_input_sort_dictionary_and_group_errors(cce_at, first):
     else:
         with pytest.raises(ValueError, match="record 10000 of input 0"):
             sort_inputs(_lib.Context(0), [a0, b])
+
+
+_SORT_LEG_NCCL = r"""
+import json, os, sys
+root = sys.argv[1]
+sys.path[:0] = [os.path.join(root, d) for d in ("hadoop-bam_amd", "tools", "oracle", "")]
+import torch, torch.distributed as dist
+import bench, sort_leg
+from hadoop_bam import _lib
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+try:
+    ctx = _lib.Context(0)
+    x = torch.ones(4, device=dev)
+    dist.all_reduce(x)  # torch's communicator before libhbam's exists
+    res = sort_leg.run(ctx, dist, 0, 1, 0.15e9, 5, 8, dev, dev, bench.N_REF, steps=1, samples=64,
+                       log=lambda *a: None)
+    dist.all_reduce(x)  # and after libhbam's was created, used and closed
+    res["torch_all_reduce"] = float(x[0])
+    print(json.dumps(res))
+finally:
+    dist.destroy_process_group()
+"""
+
+
+@pytest.mark.gpu
+def test_sort_leg_on_nccl_torch_and_libhbam_communicators_together(tmp_path):
+    """bench.py's N > 1 Sort leg (tools/sort_leg.py) on the nccl backend, world size 1: torch's
+    ProcessGroupNCCL (all_gather, broadcast of the unique id, barriers, all_reduce) and
+    libhbam's own RCCL communicator (hbam_comm_split_points, hbam_sort_exchange) live in one
+    process on one device, as on every rank of the driver's multi-GPU run (which this one-GPU
+    pool cannot rehearse with two ranks: RCCL refuses two ranks on one device).  The leg's own
+    parity (order, permutation with each record's payload, oracle sample) must be clean."""
+    import json
+    import subprocess
+    script = tmp_path / "sort_leg_nccl.py"
+    script.write_text(_SORT_LEG_NCCL)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, str(script), ROOT], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["transport"].startswith("hbam_sort_exchange"), res
+    assert res["parity"]["mismatches"] == 0, res
+    assert res["parity"]["permutation_with_own_payload"] and res["parity"]["order_key_voffset_every_rank"]
+    assert res["records"] > 0 and res["parity"]["oracle_sample"]["records"] > 0
+    assert res["stages_ms_max_over_ranks"]["exchange_rccl"] > 0
+    assert res["torch_all_reduce"] == 1.0
