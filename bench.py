@@ -629,10 +629,35 @@ def headline(args, world, elapsed, stages, huff_ms, ubytes, n_rec, own_len, file
                      "pipeline": {"bytes": int(pipe_b), "ms": round(avg["total_ms"], 3),
                                   "gb_s": round(pipe_b / (avg["total_ms"] / 1e3) / 1e9, 1),
                                   "frac": round(pipe_b / (avg["total_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                                  "what": "C + 2U + columns/pools over the whole decode"}},
+                                  "what": "C + 2U + columns/pools over the whole decode"},
+                     "issue": issue_roofline(huff_kernel)},
         "parity": parity,
     }
     return result
+
+
+# waves per SIMD each pass runs at (LDS and VGPR limits)
+WAVES_PER_SIMD = {"k_inflate_tokens": 2, "k_resolve_units": 8}
+
+
+def issue_roofline(kernel, src=os.path.join("profiles", "r06", "closing", "pmc_sq_3g.json")):
+    """The bound that actually holds the Huffman pass: instruction issue, from the committed SQ
+    counter pass of the same tree (tools/sq_fold.py).  A wave issues at most one instruction per
+    quad-cycle; a SIMD-32 runs a wave64 VALU instruction in two cycles, so its VALU pipe takes at
+    most two per quad-cycle.  None when the file is absent."""
+    try:
+        k = json.load(open(os.path.join(ROOT, src)))["kernels"][kernel]
+    except Exception:
+        return None
+    w = WAVES_PER_SIMD.get(kernel)
+    valu = k["active_inst_valu_frac"]
+    return {"kernel": kernel, "source": src, "waves_per_simd": w,
+            "wave_issue_frac": round(k["active_inst_any_frac"], 4),
+            "wave_valu_issue_frac": round(valu, 4),
+            "simd_valu_pipe_frac": round(valu * w / 2.0, 4) if w else None,
+            "wait_frac": round(k["wait_any_frac"], 4), "dependency_stall_frac": round(k["wait_inst_any_frac"], 4),
+            "what": "SQ_ACTIVE_INST_ANY / _VALU, SQ_WAIT_ANY and SQ_WAIT_INST_ANY over SQ_WAVE_CYCLES (quad-cycles) "
+                    "per wave; the SIMD's VALU pipe share = VALU issue per wave x waves per SIMD / 2"}
 
 
 if __name__ == "__main__":

@@ -140,3 +140,16 @@ def test_cpu_baseline_builds_the_same_pools_as_the_oracle_reader():
     assert n > 0 and r["records_per_s"] > 0
     assert r["pool_bytes"] == pb
     assert ("%d records" % n) in r["sample"]
+
+
+def test_issue_roofline_reads_the_committed_sq_pass():
+    """bench.py's roofline carries the instruction-issue view of the Huffman pass from the
+    committed SQ counter pass (profiles/r06/closing/pmc_sq_3g.json)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    r = bench.issue_roofline("k_inflate_tokens")
+    assert r is not None and r["waves_per_simd"] == 2
+    assert 0.0 < r["simd_valu_pipe_frac"] <= 1.0 and 0.0 < r["wave_issue_frac"] <= 1.0
+    assert abs(r["wave_issue_frac"] + r["wait_frac"] + r["dependency_stall_frac"] - 1.0) < 0.02
+    assert bench.issue_roofline("k_no_such_kernel") is None
