@@ -14,13 +14,15 @@ import __graft_entry__ as g  # noqa: E402
 
 def main():
     name, defs = sys.argv[1], sys.argv[2:]
+    # HBAM_AB_CAPI_FLAGS: extra flags for the hbam_capi.hip unit only (e.g. its own scheduler)
+    capi_extra = os.environ.get("HBAM_AB_CAPI_FLAGS", "").split()
     obj = os.path.join(ROOT, "build", "ab", name)
     os.makedirs(obj, exist_ok=True)
     cflags = [f for f in g.HIP_FLAGS if f != "-shared"] + ["-c"] + defs
     o_tok, o_capi = os.path.join(obj, "tok.o"), os.path.join(obj, "capi.o")
     procs = [subprocess.Popen([g.HIPCC] + cflags + ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-o", o_tok,
                                os.path.join(g.CSRC, "hbam_inflate_tokens.hip")]),
-             subprocess.Popen([g.HIPCC] + cflags + ["-DHBAM_SPLIT_TOK", "-o", o_capi,
+             subprocess.Popen([g.HIPCC] + cflags + capi_extra + ["-DHBAM_SPLIT_TOK", "-o", o_capi,
                                os.path.join(g.CSRC, "hbam_capi.hip")])]
     if any(p.wait() for p in procs):
         sys.exit("ab_build: compile failed")
